@@ -1,0 +1,233 @@
+"""bench.py -- BASELINE.json's headline: Mkeys/s sorting 2^30 uniform uint32 (k=8) on MI355X,
+plus the achieved HBM GB/s of the scatter pass against the roofline, and the reference's
+sequential sort (Baseline1.cu:15-64, oracle/_ref) timed on this host's cores beside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1073741824] [--k 8]
+                  [--dist uniform|zipf] [--pairs] [--rank match|split] [--no-cpu]
+
+A step = one complete sort of the resident input (every pass: histogram, scan, fused local
+sort + scatter), device-resident: inputs are generated in HBM before timing, the timed region
+is K back-to-back sorts bracketed by barrier + synchronize. N>1 (launched by
+torch.distributed.run, one process per GPU over RCCL): each rank holds n keys of one global
+uniform stream (block-distributed), and a step is the full multi-GPU sort (histogram
+all-reduce, partition, one all-to-all over xGMI, local sort) -> weak scaling.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "cuda.radixsort_amd"))
+import radixsort as rs  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1 << 30)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--pairs", action="store_true")
+    ap.add_argument("--rank", choices=["match", "split"], default="match")
+    ap.add_argument("--tiles-per-chunk", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--vendor", action="store_true", help="also time rocPRIM's radix sort")
+    return ap.parse_args()
+
+
+def traffic_for(config_key: str):
+    """HBM bytes per scatter launch from the committed PMC profile (profiles/*pmc*.json), or None."""
+    for f in sorted((ROOT / "profiles").glob("*pmc*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        rec = d.get("configs", {}).get(config_key)
+        if rec and rec.get("hbm_bytes_per_launch"):
+            return rec["hbm_bytes_per_launch"], f.name
+    return None, None
+
+
+def cpu_baseline(n, k, reps, dist):
+    """Baseline1's sortByHost on this host, single thread: the reference's own code from
+    oracle/_ref when it was built (kind "reference"), else the oracle port (kind "port")."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _util  # test/bench infrastructure: the oracle loaders (never the product path)
+    x = _util.uniform_keys(n) if dist == "uniform" else _util.zipf_keys(n)
+    out = np.empty_like(x)
+    ref = _util.ref_lib()
+    if ref is not None:
+        kind = "reference"
+        fn = lambda: ref.ref_sort_by_host(_util._ptr(x), n, _util._ptr(out), k)  # noqa: E731
+    else:
+        kind = "port"
+        fn = lambda: _util.oracle().oracle_sort_by_host(_util._ptr(x), n, _util._ptr(out), k)  # noqa: E731
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(n / med / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": kind,
+            "sample": f"{n} {dist} u32 keys, k={k}, median of {reps} single-thread runs "
+                      f"({med * 1e3:.0f} ms each) of Baseline1 sortByHost on {model or 'host CPU'} "
+                      f"(host has {os.cpu_count()} logical CPUs)",
+            "ms_per_sort": round(med * 1e3, 2)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
+
+    n = a.n
+    seed = 0x5EED + rank * n  # one global splitmix stream, block-distributed by index
+    keys = rs.empty_u32(n, dev)
+    if a.dist == "uniform":
+        rs.gen_uniform(keys, seed)
+    else:
+        sys.path.insert(0, str(ROOT / "tests"))
+        from _util import zipf_cdf_u32
+        rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32(), dev), seed)
+    vals = None
+    if a.pairs:
+        vals = rs.empty_u32(n, dev)
+        rs.gen_iota(vals, rank * n)
+    out = rs.empty_u32(n, dev)
+    vout = rs.empty_u32(n, dev) if a.pairs else None
+    p = rs.plan(n, a.k, a.pairs, a.tiles_per_chunk)
+    ws = rs.workspace(p.workspace_bytes, dev)
+
+    if world > 1:
+        import multi
+        ops = multi.GpuOps(dev)
+
+        def step():
+            return multi.dist_sort(keys, a.k, vals=vals, ops=ops)
+    else:
+        def step():
+            rs.sort_device(keys, out, a.k, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    with rs.Profile() as prof:
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    barrier()
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # per-kernel: the fused local-sort + scatter pass (the dominant kernel)
+    sc = prof.times["scatter"]
+    hi = prof.times["histogram"]
+    scan = prof.times["scan"]
+    bytes_per_key = 16 if a.pairs else 8
+    scatter_ms = sc["ms"] / max(1, sc["launches"])
+    keys_per_launch = sc["keys"] / max(1, sc["launches"])
+    achieved = bytes_per_key * keys_per_launch / (scatter_ms * 1e-3) / 1e9
+    cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}"
+    traffic, traffic_src = traffic_for(cfg_key)
+
+    vendor = None
+    if a.vendor and world == 1:
+        vo = rs.empty_u32(n, dev)
+        vws = rs.workspace(int(rs._lib().rsort_vendor_workspace_size(n)), dev)
+        rs.vendor_sort_device(keys, vo, ws=vws)
+        torch.cuda.synchronize()
+        tv = time.perf_counter()
+        for _ in range(a.steps):
+            rs.vendor_sort_device(keys, vo, ws=vws)
+        torch.cuda.synchronize()
+        tv = (time.perf_counter() - tv) / a.steps
+        vendor = {"value": round(n / tv / 1e6, 1), "unit": "Mkeys/s", "ms_per_sort": round(tv * 1e3, 3),
+                  "impl": "rocprim::radix_sort_keys"}
+        del vo, vws
+
+    if rank == 0:
+        total_keys = n * world * a.steps
+        line = {
+            "metric": "Mkeys/s sorting 2^30 uniform uint32; scatter-pass achieved HBM GB/s",
+            "value": round(total_keys / elapsed / 1e6, 1),
+            "unit": "Mkeys/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (splitmix64 uniform u32, seed 0x5EED, generated in HBM)"
+                    if a.dist == "uniform" else "synthetic (Zipf s=1.0 over 2^20 ranks, key=fmix32(rank))",
+            "config": {"workload": f"sort {n} {'key+value pairs' if a.pairs else 'uint32 keys'} per GPU, "
+                                   f"k={a.k} ({p.passes} passes), {a.dist}",
+                       "keys_per_gpu": n, "k_bits": a.k, "passes": p.passes, "dist": a.dist,
+                       "pairs": bool(a.pairs), "rank_algo": a.rank, "tile_keys": p.tile_keys,
+                       "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
+                       "parallelism": "single GPU" if world == 1 else f"range-partition x{world} (RCCL all-to-all)"},
+            "roofline": {"bound": "hbm", "kernel": "rs_scatter (fused local sort + rank + scatter)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": int(bytes_per_key * keys_per_launch),
+                         "avg_launch_ms": round(scatter_ms, 4)},
+            "phases_ms_per_step": {"histogram": round(hi["ms"] / a.steps, 4), "scan": round(scan["ms"] / a.steps, 4),
+                                   "scatter": round(sc["ms"] / a.steps, 4)},
+        }
+        if vendor:
+            line["vendor"] = vendor
+        if world == 1 and not a.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(min(a.cpu_n, n), a.k, a.cpu_reps, a.dist)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

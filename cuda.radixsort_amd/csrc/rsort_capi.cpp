@@ -1,0 +1,578 @@
+// rsort_capi.cpp -- host driver + C ABI (include/rsort.h) of the gfx950 LSD radix sort.
+//
+// Replaces the reference's per-digit driver sortByDevice (Parallel7.cu:530-639) and the
+// dispatcher's device branch (Parallel7.cu:641-662). Differences by design:
+//   * workspace is planned once (rsort_plan) and passed in, not cudaMalloc'ed per call or
+//     kept in function statics (P7:203-218, :489-505); the host entry caches one per device;
+//   * one stream, no host synchronisation inside the pass loop (P7 syncs after every launch
+//     and round-trips the block sums through the host every pass, P7:224-235, :514-519);
+//   * errors are returned as rsort_status, never exit() (common.h:6-16).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "rsort.h"
+#include "rsort_internal.hpp"
+
+using namespace rsort;
+
+namespace {
+
+constexpr int kVersion = 100;  // 0.1.0
+std::atomic<int> g_rank_algo{RSORT_RANK_MATCH};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// ------------------------------------------------------------------------------ profiler
+struct ProfRec {
+    int phase;
+    int64_t keys;
+    hipEvent_t a, b;
+};
+
+struct Profiler {
+    std::mutex mu;
+    bool on = false;
+    std::vector<ProfRec> recs;
+    std::vector<hipEvent_t> pool;
+
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+};
+Profiler g_prof;
+
+// RAII scope: records a start event now and a stop event on destruction (same stream).
+struct PhaseScope {
+    bool active = false;
+    ProfRec rec{};
+    hipStream_t s;
+    PhaseScope(int phase, int64_t keys, hipStream_t stream) : s(stream) {
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        if (!g_prof.on) return;
+        rec.phase = phase;
+        rec.keys = keys;
+        rec.a = g_prof.get();
+        rec.b = g_prof.get();
+        if (!rec.a || !rec.b) return;
+        if (hipEventRecord(rec.a, s) != hipSuccess) return;
+        active = true;
+    }
+    ~PhaseScope() {
+        if (!active) return;
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        if (hipEventRecord(rec.b, s) == hipSuccess) g_prof.recs.push_back(rec);
+    }
+};
+
+int hip_status(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP; }
+
+bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
+
+// ------------------------------------------------------------------------------ planning
+int device_shape(int bits, int pairs, int *cus, int *bpc) {
+    *cus = 256;
+    *bpc = 4;
+    int dev = 0, count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+        *cus = c;
+    const int b = scatter_blocks_per_cu(bits, pairs, g_rank_algo.load());
+    if (b > 0) *bpc = b;
+    return 1;
+}
+
+int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p) {
+    if (!p) return RSORT_ERR_ARG;
+    if (k < kMinBits || k > kMaxBits) return RSORT_ERR_BITS;
+    if (n < 0 || n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (tpc < 0) return RSORT_ERR_ARG;
+    memset(p, 0, sizeof(*p));
+    p->n = n;
+    p->k_bits = k;
+    p->passes = (32 + k - 1) / k;
+    p->bins = 1 << k;
+    p->threads = kThreads;
+    p->tile_keys = kTileKeys;
+    p->pairs = pairs ? 1 : 0;
+    const int64_t tiles = std::max<int64_t>(1, (n + kTileKeys - 1) / kTileKeys);
+    if (tpc == 0) {
+        int cus, bpc;
+        device_shape(k, pairs, &cus, &bpc);
+        const int64_t target = std::max<int64_t>(1, (int64_t)cus * bpc);
+        tpc = (tiles + target - 1) / target;
+    }
+    p->tiles_per_chunk = tpc;
+    p->chunk_keys = tpc * kTileKeys;
+    p->num_chunks = (tiles + tpc - 1) / tpc;
+    p->table_entries = (int64_t)p->bins * p->num_chunks;
+    p->scan_blocks = (p->table_entries + kScanSegment - 1) / kScanSegment;
+    size_t ws = align256((size_t)n * 4);                     // ping-pong keys
+    if (pairs) ws += align256((size_t)n * 4);                // ping-pong values
+    ws += align256((size_t)p->table_entries * 4);            // chunk x digit table
+    ws += align256((size_t)p->scan_blocks * 4);              // scan block sums
+    ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
+    p->workspace_bytes = ws;
+    return RSORT_OK;
+}
+
+struct Carve {
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts;
+};
+
+Carve carve(const rsort_plan &p, void *ws) {
+    Carve c{};
+    char *q = (char *)ws;
+    c.tmp_k = (uint32_t *)q;
+    q += align256((size_t)p.n * 4);
+    if (p.pairs) {
+        c.tmp_v = (uint32_t *)q;
+        q += align256((size_t)p.n * 4);
+    }
+    c.table = (uint32_t *)q;
+    q += align256((size_t)p.table_entries * 4);
+    c.bsums = (uint32_t *)q;
+    q += align256((size_t)p.scan_blocks * 4);
+    c.starts = (uint32_t *)q;
+    return c;
+}
+
+// ------------------------------------------------------------------------------ pass pieces
+int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
+                 int dmode, const uint32_t *split, int nsplit, hipStream_t s) {
+    HistArgs a{};
+    a.keys = keys;
+    a.table = table;
+    a.n = (uint64_t)p.n;
+    a.chunk_keys = (uint64_t)p.chunk_keys;
+    a.num_chunks = (uint32_t)p.num_chunks;
+    a.shift = (uint32_t)shift;
+    a.vec = (((uintptr_t)keys & 15u) == 0) ? 1u : 0u;
+    a.nsplit = (uint32_t)nsplit;
+    for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
+    PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
+    return hip_status(launch_histogram(p.k_bits, dmode, a, s));
+}
+
+int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s) {
+    ScanArgs a{};
+    a.table = table;
+    a.block_sums = bsums;
+    a.m = (uint64_t)p.table_entries;
+    a.nblocks = (uint32_t)p.scan_blocks;
+    PhaseScope ps(RSORT_PHASE_SCAN, p.table_entries, s);
+    return hip_status(launch_scan(a, s));
+}
+
+int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
+               uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
+               const uint32_t *split, int nsplit, hipStream_t s) {
+    ScatterArgs a{};
+    a.kin = kin;
+    a.vin = vin;
+    a.kout = kout;
+    a.vout = vout;
+    a.table = table;
+    a.n = (uint64_t)p.n;
+    a.chunk_keys = (uint64_t)p.chunk_keys;
+    a.num_chunks = (uint32_t)p.num_chunks;
+    a.shift = (uint32_t)shift;
+    a.local_only = local_only ? 1u : 0u;
+    a.nsplit = (uint32_t)nsplit;
+    for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
+    const int rank = (dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH;
+    PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
+    return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, a, s));
+}
+
+int check_plan(const rsort_plan *p) {
+    if (!p) return RSORT_ERR_ARG;
+    if (p->k_bits < kMinBits || p->k_bits > kMaxBits) return RSORT_ERR_BITS;
+    if (p->n < 0 || p->n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (p->tiles_per_chunk <= 0 || p->num_chunks <= 0 ||
+        p->num_chunks * p->tiles_per_chunk * kTileKeys < p->n ||
+        p->chunk_keys != p->tiles_per_chunk * kTileKeys || p->bins != (1 << p->k_bits) ||
+        p->table_entries != (int64_t)p->bins * p->num_chunks)
+        return RSORT_ERR_ARG;
+    return RSORT_OK;
+}
+
+int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
+                 uint32_t *vout, void *ws, size_t wsb, hipStream_t s) {
+    int st = check_plan(&p);
+    if (st) return st;
+    if (p.n == 0) return RSORT_OK;
+    if (!kin || !kout || !ws || (p.pairs && (!vin || !vout))) return RSORT_ERR_ARG;
+    if (!aligned4(kin) || !aligned4(kout) || (p.pairs && (!aligned4(vin) || !aligned4(vout))))
+        return RSORT_ERR_ALIGN;
+    if (wsb < p.workspace_bytes) return RSORT_ERR_WORKSPACE;
+    const Carve c = carve(p, ws);
+    const int P = p.passes;
+    const uint32_t *sk = kin, *sv = vin;
+    const bool inplace = (kin == kout) || (p.pairs && vin == vout);
+    if (inplace && (P % 2 == 1)) {
+        // pass 0 must not read the buffer it writes: stage the input in the ping-pong buffer
+        PhaseScope ps(RSORT_PHASE_COPY, p.n, s);
+        if (hipMemcpyAsync(c.tmp_k, kin, (size_t)p.n * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+        if (p.pairs &&
+            hipMemcpyAsync(c.tmp_v, vin, (size_t)p.n * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+        sk = c.tmp_k;
+        sv = c.tmp_v;
+    }
+    for (int i = 0; i < P; ++i) {
+        const int shift = i * p.k_bits;
+        const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
+        uint32_t *dk = to_out ? kout : c.tmp_k;
+        uint32_t *dv = to_out ? vout : c.tmp_v;
+        if ((st = do_histogram(p, sk, shift, c.table, kDigitShift, nullptr, 0, s))) return st;
+        if ((st = do_scan(p, c.table, c.bsums, s))) return st;
+        if ((st = do_scatter(p, sk, sv, dk, dv, shift, c.table, 0, kDigitShift, nullptr, 0, s)))
+            return st;
+        sk = dk;
+        sv = dv;
+    }
+    return RSORT_OK;
+}
+
+// ------------------------------------------------------------------------------ host entry cache
+struct DevCache {
+    std::mutex mu;
+    int device = -1;
+    void *buf = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+std::mutex g_cache_mu;
+std::vector<DevCache *> g_caches;
+
+DevCache *cache_for(int dev) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (DevCache *c : g_caches)
+        if (c->device == dev) return c;
+    DevCache *c = new DevCache();
+    c->device = dev;
+    g_caches.push_back(c);
+    return c;
+}
+
+int host_sort(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout,
+              int64_t n, int k, rsort_phase_times *times) {
+    const int pairs = vin != nullptr;
+    rsort_plan p;
+    int st = plan_fill(n, k, pairs, 0, &p);
+    if (st) return st;
+    if (n == 0) {
+        if (times) memset(times, 0, sizeof(*times));
+        return RSORT_OK;
+    }
+    if (!kin || !kout || (pairs && !vout)) return RSORT_ERR_ARG;
+    int count = 0, dev = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return RSORT_ERR_NODEV;
+    if (hipGetDevice(&dev) != hipSuccess) return RSORT_ERR_HIP;
+    DevCache *dc = cache_for(dev);
+    std::lock_guard<std::mutex> g(dc->mu);
+    const size_t nb = align256((size_t)n * 4);
+    const size_t need = nb * (pairs ? 4 : 2) + p.workspace_bytes;
+    if (!dc->stream && hipStreamCreateWithFlags(&dc->stream, hipStreamNonBlocking) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (dc->cap < need) {
+        if (dc->buf) (void)hipFree(dc->buf);
+        dc->buf = nullptr;
+        dc->cap = 0;
+        if (hipMalloc(&dc->buf, need) != hipSuccess) return RSORT_ERR_ALLOC;
+        dc->cap = need;
+    }
+    char *q = (char *)dc->buf;
+    uint32_t *d_kin = (uint32_t *)q;
+    uint32_t *d_kout = (uint32_t *)(q + nb);
+    uint32_t *d_vin = pairs ? (uint32_t *)(q + 2 * nb) : nullptr;
+    uint32_t *d_vout = pairs ? (uint32_t *)(q + 3 * nb) : nullptr;
+    void *ws = q + nb * (pairs ? 4 : 2);
+    hipStream_t s = dc->stream;
+    if (hipMemcpyAsync(d_kin, kin, (size_t)n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (pairs && hipMemcpyAsync(d_vin, vin, (size_t)n * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (times) rsort_profile_begin();
+    st = sort_planned(p, d_kin, d_vin, d_kout, d_vout, ws, p.workspace_bytes, s);
+    if (times) {
+        const int st2 = rsort_profile_end(times);
+        if (!st) st = st2;
+    }
+    if (st) {
+        (void)hipStreamSynchronize(s);
+        return st;
+    }
+    if (hipMemcpyAsync(kout, d_kout, (size_t)n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (pairs && hipMemcpyAsync(vout, d_vout, (size_t)n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    return hip_status(hipStreamSynchronize(s));
+}
+
+}  // namespace
+
+// ================================================================================ C ABI
+extern "C" {
+
+const char *rsort_status_string(int status) {
+    switch (status) {
+        case RSORT_OK: return "ok";
+        case RSORT_ERR_ARG: return "invalid argument";
+        case RSORT_ERR_BITS: return "k_bits outside [1, 12]";
+        case RSORT_ERR_SIZE: return "n outside [0, 2^32)";
+        case RSORT_ERR_ALIGN: return "device buffer not 4-byte aligned";
+        case RSORT_ERR_ALLOC: return "allocation failed";
+        case RSORT_ERR_HIP: return "HIP runtime error";
+        case RSORT_ERR_WORKSPACE: return "workspace too small";
+        case RSORT_ERR_NODEV: return "no HIP device";
+        default: return "unknown status";
+    }
+}
+
+int rsort_version(void) { return kVersion; }
+
+int rsort_plan_make(int64_t n, int k_bits, int pairs, int64_t tiles_per_chunk, rsort_plan *plan) {
+    return plan_fill(n, k_bits, pairs, tiles_per_chunk, plan);
+}
+
+size_t rsort_workspace_size(int64_t n, int k_bits, int pairs) {
+    rsort_plan p;
+    if (plan_fill(n, k_bits, pairs, 0, &p) != RSORT_OK) return 0;
+    return p.workspace_bytes;
+}
+
+int rsort_sort_planned(const rsort_plan *plan, const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                       uint32_t *d_keys_out, uint32_t *d_vals_out, void *d_workspace,
+                       size_t workspace_bytes, void *stream) {
+    if (!plan) return RSORT_ERR_ARG;
+    return sort_planned(*plan, d_keys_in, d_vals_in, d_keys_out, d_vals_out, d_workspace,
+                        workspace_bytes, (hipStream_t)stream);
+}
+
+int rsort_u32_device(const uint32_t *d_in, uint32_t *d_out, int64_t n, int k_bits,
+                     void *d_workspace, size_t workspace_bytes, void *stream) {
+    rsort_plan p;
+    const int st = plan_fill(n, k_bits, 0, 0, &p);
+    if (st) return st;
+    return sort_planned(p, d_in, nullptr, d_out, nullptr, d_workspace, workspace_bytes,
+                        (hipStream_t)stream);
+}
+
+int rsort_u32_pairs_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                           uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t n, int k_bits,
+                           void *d_workspace, size_t workspace_bytes, void *stream) {
+    rsort_plan p;
+    const int st = plan_fill(n, k_bits, 1, 0, &p);
+    if (st) return st;
+    return sort_planned(p, d_keys_in, d_vals_in, d_keys_out, d_vals_out, d_workspace,
+                        workspace_bytes, (hipStream_t)stream);
+}
+
+int rsort_u32(const uint32_t *in, uint32_t *out, int64_t n, int k_bits) {
+    return host_sort(in, nullptr, out, nullptr, n, k_bits, nullptr);
+}
+
+int rsort_u32_ex(const uint32_t *in, uint32_t *out, int64_t n, int k_bits, int block_size,
+                 rsort_phase_times *times) {
+    (void)block_size;
+    return host_sort(in, nullptr, out, nullptr, n, k_bits, times);
+}
+
+int rsort_u32_pairs(const uint32_t *keys_in, const uint32_t *vals_in, uint32_t *keys_out,
+                    uint32_t *vals_out, int64_t n, int k_bits) {
+    if (n > 0 && (!vals_in || !vals_out)) return RSORT_ERR_ARG;
+    return host_sort(keys_in, vals_in, keys_out, vals_out, n, k_bits, nullptr);
+}
+
+int rsort_pass_histogram(const rsort_plan *plan, const uint32_t *d_keys, int shift,
+                         uint32_t *d_table, void *stream) {
+    int st = check_plan(plan);
+    if (st) return st;
+    if (shift < 0 || shift > 31) return RSORT_ERR_ARG;
+    if (plan->n == 0) return RSORT_OK;
+    if (!d_keys || !d_table) return RSORT_ERR_ARG;
+    return do_histogram(*plan, d_keys, shift, d_table, kDigitShift, nullptr, 0, (hipStream_t)stream);
+}
+
+int rsort_pass_scan(const rsort_plan *plan, uint32_t *d_table, uint32_t *d_block_sums, void *stream) {
+    int st = check_plan(plan);
+    if (st) return st;
+    if (plan->n == 0) return RSORT_OK;
+    if (!d_table || !d_block_sums) return RSORT_ERR_ARG;
+    return do_scan(*plan, d_table, d_block_sums, (hipStream_t)stream);
+}
+
+int rsort_pass_scatter(const rsort_plan *plan, const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                       uint32_t *d_keys_out, uint32_t *d_vals_out, int shift, const uint32_t *d_table,
+                       void *stream) {
+    int st = check_plan(plan);
+    if (st) return st;
+    if (shift < 0 || shift > 31) return RSORT_ERR_ARG;
+    if (plan->n == 0) return RSORT_OK;
+    if (!d_keys_in || !d_keys_out || !d_table || (plan->pairs && (!d_vals_in || !d_vals_out)))
+        return RSORT_ERR_ARG;
+    return do_scatter(*plan, d_keys_in, d_vals_in, d_keys_out, d_vals_out, shift, d_table, 0,
+                      kDigitShift, nullptr, 0, (hipStream_t)stream);
+}
+
+int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                          uint32_t *d_keys_out, uint32_t *d_vals_out, int shift, void *stream) {
+    int st = check_plan(plan);
+    if (st) return st;
+    if (shift < 0 || shift > 31) return RSORT_ERR_ARG;
+    if (plan->n == 0) return RSORT_OK;
+    if (!d_keys_in || !d_keys_out || (plan->pairs && (!d_vals_in || !d_vals_out)))
+        return RSORT_ERR_ARG;
+    if (d_keys_in == d_keys_out) return RSORT_ERR_ARG;
+    // local-only mode never reads the offset table
+    const uint32_t *table = nullptr;
+    return do_scatter(*plan, d_keys_in, d_vals_in, d_keys_out, d_vals_out, shift, table, 1,
+                      kDigitShift, nullptr, 0, (hipStream_t)stream);
+}
+
+int rsort_set_rank_algo(int algo) {
+    if (algo != RSORT_RANK_MATCH && algo != RSORT_RANK_SPLIT) return RSORT_ERR_ARG;
+    g_rank_algo.store(algo);
+    return RSORT_OK;
+}
+
+int rsort_get_rank_algo(void) { return g_rank_algo.load(); }
+
+int rsort_profile_begin(void) {
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    for (auto &r : g_prof.recs) {
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.recs.clear();
+    g_prof.on = true;
+    return RSORT_OK;
+}
+
+int rsort_profile_end(rsort_phase_times *out) {
+    std::vector<ProfRec> recs;
+    {
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        g_prof.on = false;
+        recs.swap(g_prof.recs);
+    }
+    rsort_phase_times t;
+    memset(&t, 0, sizeof(t));
+    int st = RSORT_OK;
+    for (auto &r : recs) {
+        if (hipEventSynchronize(r.b) != hipSuccess) {
+            st = RSORT_ERR_HIP;
+            continue;
+        }
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) {
+            st = RSORT_ERR_HIP;
+            continue;
+        }
+        t.ms[r.phase] += ms;
+        t.launches[r.phase] += 1;
+        t.keys[r.phase] += r.keys;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_prof.mu);
+        for (auto &r : recs) {
+            g_prof.pool.push_back(r.a);
+            g_prof.pool.push_back(r.b);
+        }
+    }
+    if (out) *out = t;
+    return st;
+}
+
+int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in, uint32_t *d_keys_out,
+                           uint32_t *d_vals_out, int64_t n, const uint32_t *splitters, int num_buckets,
+                           uint32_t *d_bucket_starts, void *d_workspace, size_t workspace_bytes,
+                           void *stream) {
+    if (num_buckets < 1 || num_buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;
+    if (num_buckets > 1 && !splitters) return RSORT_ERR_ARG;
+    for (int i = 1; i + 1 < num_buckets; ++i)
+        if (splitters[i] < splitters[i - 1]) return RSORT_ERR_ARG;
+    int bits = 1;
+    while ((1 << bits) < num_buckets) ++bits;
+    const int pairs = d_vals_in != nullptr;
+    rsort_plan p;
+    int st = plan_fill(n, bits, pairs, 0, &p);
+    if (st) return st;
+    if (!d_bucket_starts) return RSORT_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        return hip_status(hipMemsetAsync(d_bucket_starts, 0, (size_t)(num_buckets + 1) * 4, s));
+    }
+    if (!d_keys_in || !d_keys_out || !d_workspace || (pairs && !d_vals_out)) return RSORT_ERR_ARG;
+    if (d_keys_in == d_keys_out) return RSORT_ERR_ARG;
+    if (workspace_bytes < p.workspace_bytes) return RSORT_ERR_WORKSPACE;
+    const Carve c = carve(p, d_workspace);
+    const int ns = num_buckets - 1;
+    if ((st = do_histogram(p, d_keys_in, 0, c.table, kDigitSplit, splitters, ns, s))) return st;
+    if ((st = do_scan(p, c.table, c.bsums, s))) return st;
+    if ((st = do_scatter(p, d_keys_in, d_vals_in, d_keys_out, d_vals_out, 0, c.table, 0, kDigitSplit,
+                         splitters, ns, s)))
+        return st;
+    return hip_status(launch_gather_starts(c.table, (uint32_t)p.num_chunks, (uint32_t)num_buckets,
+                                           (uint64_t)n, d_bucket_starts, s));
+}
+
+int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits, uint32_t *d_hist,
+                        void *d_workspace, size_t workspace_bytes, void *stream) {
+    rsort_plan p;
+    int st = plan_fill(n, top_bits, 0, 0, &p);
+    if (st) return st;
+    if (!d_hist) return RSORT_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return hip_status(hipMemsetAsync(d_hist, 0, (size_t)p.bins * 4, s));
+    if (!d_keys || !d_workspace) return RSORT_ERR_ARG;
+    if (workspace_bytes < p.workspace_bytes) return RSORT_ERR_WORKSPACE;
+    const Carve c = carve(p, d_workspace);
+    if ((st = do_histogram(p, d_keys, 32 - top_bits, c.table, kDigitShift, nullptr, 0, s))) return st;
+    if ((st = do_scan(p, c.table, c.bsums, s))) return st;
+    hipError_t e = launch_gather_starts(c.table, (uint32_t)p.num_chunks, (uint32_t)p.bins,
+                                        (uint64_t)n, c.starts, s);
+    if (e != hipSuccess) return RSORT_ERR_HIP;
+    return hip_status(launch_diff_starts(c.starts, (uint32_t)p.bins, d_hist, s));
+}
+
+int rsort_gen_uniform(uint32_t *d_out, int64_t n, uint64_t seed, void *stream) {
+    if (n < 0) return RSORT_ERR_SIZE;
+    if (n == 0) return RSORT_OK;
+    if (!d_out) return RSORT_ERR_ARG;
+    return hip_status(launch_gen_uniform(d_out, (uint64_t)n, seed, (hipStream_t)stream));
+}
+
+int rsort_gen_zipf(uint32_t *d_out, int64_t n, uint64_t seed, const uint32_t *d_cdf, int64_t ranks,
+                   void *stream) {
+    if (n < 0) return RSORT_ERR_SIZE;
+    if (n == 0) return RSORT_OK;
+    if (!d_out || !d_cdf || ranks <= 0) return RSORT_ERR_ARG;
+    return hip_status(launch_gen_zipf(d_out, (uint64_t)n, seed, d_cdf, (uint64_t)ranks, (hipStream_t)stream));
+}
+
+int rsort_gen_iota(uint32_t *d_out, int64_t n, uint32_t base, void *stream) {
+    if (n < 0) return RSORT_ERR_SIZE;
+    if (n == 0) return RSORT_OK;
+    if (!d_out) return RSORT_ERR_ARG;
+    return hip_status(launch_gen_iota(d_out, (uint64_t)n, base, (hipStream_t)stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// rsort_internal.hpp -- shared between the HIP kernels (rsort_kernels.hip) and the host
+// driver (rsort_capi.cpp). Not part of the public ABI (include/rsort.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsort {
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;              // workgroup size of every pass kernel
+constexpr int kKeysPerThread = 16;         // keys per thread per tile
+constexpr int kTileKeys = kThreads * kKeysPerThread;  // 4096 keys = 16 KiB per tile
+constexpr int kMinBits = 1;
+constexpr int kMaxBits = 12;
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 16;
+constexpr int kScanSegment = kScanThreads * kScanPerThread;  // table entries per scan block
+constexpr int kMaxSplitters = 15;          // partition: <= 16 buckets
+
+enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
+
+struct HistArgs {
+    const uint32_t *keys;
+    uint32_t *table;        // [bins][num_chunks]
+    uint64_t n;
+    uint64_t chunk_keys;
+    uint32_t num_chunks;
+    uint32_t shift;
+    uint32_t vec;           // keys 16-byte aligned: uint4 loads
+    uint32_t nsplit;
+    uint32_t splitters[kMaxSplitters];
+};
+
+struct ScatterArgs {
+    const uint32_t *kin;
+    const uint32_t *vin;
+    uint32_t *kout;
+    uint32_t *vout;
+    const uint32_t *table;  // scanned [bins][num_chunks]
+    uint64_t n;
+    uint64_t chunk_keys;
+    uint32_t num_chunks;
+    uint32_t shift;
+    uint32_t local_only;    // 1: write each tile's local order back in place of the tile
+    uint32_t nsplit;
+    uint32_t splitters[kMaxSplitters];
+};
+
+struct ScanArgs {
+    uint32_t *table;
+    uint32_t *block_sums;
+    uint64_t m;             // table entries
+    uint32_t nblocks;
+};
+
+// Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.
+hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t s);
+hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, const ScatterArgs &a,
+                          hipStream_t s);
+hipError_t launch_scan(const ScanArgs &a, hipStream_t s);
+hipError_t launch_gather_starts(const uint32_t *table, uint32_t num_chunks, uint32_t bins,
+                                uint64_t n, uint32_t *starts, hipStream_t s);
+hipError_t launch_diff_starts(const uint32_t *starts, uint32_t bins, uint32_t *hist,
+                              hipStream_t s);
+hipError_t launch_gen_uniform(uint32_t *out, uint64_t n, uint64_t seed, hipStream_t s);
+hipError_t launch_gen_zipf(uint32_t *out, uint64_t n, uint64_t seed, const uint32_t *cdf,
+                           uint64_t ranks, hipStream_t s);
+hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t s);
+// Resident scatter workgroups per CU (occupancy query), 0 on error.
+int scatter_blocks_per_cu(int bits, int pairs, int rank_algo);
+
+}  // namespace rsort

@@ -1,0 +1,368 @@
+"""Python host mirror of the reference's sort interface, over the C ABI (include/rsort.h).
+
+Names and argument meaning follow truongchauhien/CUDA.RadixSort (Parallel7.cu):
+  Implementation                 enum {SORT_BY_HOST, SORT_BY_THRUST, SORT_BY_DEVICE}  (P7:22)
+  sort(in, n, out, implementation, numBits, blockSize)                              (P7:641-662)
+  sortByDevice(h_input, n, h_output, numBits, blockSize)                            (P7:530-639)
+  sortByThrust(input, n, output)                                                   (P7:69-73)
+plus device-resident entry points over torch tensors (torch is plumbing: device memory and
+streams only) and the per-pass building blocks used by the parity tests.
+
+Error behaviour: the reference prints and exit(EXIT_FAILURE)s on any CUDA error
+(common.h:6-16); here every non-zero rsort_status raises RSortError carrying the status.
+
+There is NO CPU fallback: the library must be built (python cuda.radixsort_amd/build.py) and
+a HIP device visible, otherwise these functions raise. SORT_BY_HOST, the reference's
+sequential CPU sort, is not part of this library (it is the test oracle, oracle/; the C++
+compat header include/radixsort.hpp offers it to C++ callers of the reference API).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import time
+from contextlib import contextmanager
+from pathlib import Path
+
+import numpy as np
+
+try:  # load torch first so librsort binds to the same HIP runtime instance
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the host->host API
+    torch = None
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "librsort.so"
+
+RSORT_OK = 0
+STATUS_NAMES = {0: "RSORT_OK", 1: "RSORT_ERR_ARG", 2: "RSORT_ERR_BITS", 3: "RSORT_ERR_SIZE",
+                4: "RSORT_ERR_ALIGN", 5: "RSORT_ERR_ALLOC", 6: "RSORT_ERR_HIP",
+                7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV"}
+RANK_MATCH, RANK_SPLIT = 0, 1
+PHASES = ("histogram", "scan", "scatter", "copy")
+
+
+class Implementation(enum.IntEnum):
+    SORT_BY_HOST = 0
+    SORT_BY_THRUST = 1
+    SORT_BY_DEVICE = 2
+
+
+SORT_BY_HOST = Implementation.SORT_BY_HOST
+SORT_BY_THRUST = Implementation.SORT_BY_THRUST
+SORT_BY_DEVICE = Implementation.SORT_BY_DEVICE
+
+
+class RSortError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        self.status = status
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)} ({_lib().rsort_status_string(status).decode()})")
+
+
+class Plan(ctypes.Structure):
+    """rsort_plan (include/rsort.h)."""
+    _fields_ = [("n", ctypes.c_int64), ("k_bits", ctypes.c_int32), ("passes", ctypes.c_int32),
+                ("bins", ctypes.c_int32), ("threads", ctypes.c_int32), ("tile_keys", ctypes.c_int32),
+                ("pairs", ctypes.c_int32), ("tiles_per_chunk", ctypes.c_int64),
+                ("chunk_keys", ctypes.c_int64), ("num_chunks", ctypes.c_int64),
+                ("table_entries", ctypes.c_int64), ("scan_blocks", ctypes.c_int64),
+                ("workspace_bytes", ctypes.c_size_t)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class PhaseTimes(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double * 4), ("launches", ctypes.c_int64 * 4), ("keys", ctypes.c_int64 * 4)]
+
+    def as_dict(self):
+        return {p: {"ms": self.ms[i], "launches": self.launches[i], "keys": self.keys[i]}
+                for i, p in enumerate(PHASES)}
+
+
+# Every symbol include/rsort.h declares, with its ctypes signature.
+_u32p, _vp, _i64, _int, _sz = (ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.c_int, ctypes.c_size_t)
+_PP = ctypes.POINTER(Plan)
+SIGNATURES = {
+    "rsort_status_string": ([_int], ctypes.c_char_p),
+    "rsort_version": ([], _int),
+    "rsort_plan_make": ([_i64, _int, _int, _i64, _PP], _int),
+    "rsort_workspace_size": ([_i64, _int, _int], _sz),
+    "rsort_u32_device": ([_vp, _vp, _i64, _int, _vp, _sz, _vp], _int),
+    "rsort_u32_pairs_device": ([_vp, _vp, _vp, _vp, _i64, _int, _vp, _sz, _vp], _int),
+    "rsort_sort_planned": ([_PP, _vp, _vp, _vp, _vp, _vp, _sz, _vp], _int),
+    "rsort_u32": ([_vp, _vp, _i64, _int], _int),
+    "rsort_u32_ex": ([_vp, _vp, _i64, _int, _int, ctypes.POINTER(PhaseTimes)], _int),
+    "rsort_u32_pairs": ([_vp, _vp, _vp, _vp, _i64, _int], _int),
+    "rsort_pass_histogram": ([_PP, _vp, _int, _vp, _vp], _int),
+    "rsort_pass_scan": ([_PP, _vp, _vp, _vp], _int),
+    "rsort_pass_scatter": ([_PP, _vp, _vp, _vp, _vp, _int, _vp, _vp], _int),
+    "rsort_pass_local_sort": ([_PP, _vp, _vp, _vp, _vp, _int, _vp], _int),
+    "rsort_set_rank_algo": ([_int], _int),
+    "rsort_get_rank_algo": ([], _int),
+    "rsort_profile_begin": ([], _int),
+    "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
+    "rsort_partition_device": ([_vp, _vp, _vp, _vp, _i64, _u32p, _int, _vp, _vp, _sz, _vp], _int),
+    "rsort_top_histogram": ([_vp, _i64, _int, _vp, _vp, _sz, _vp], _int),
+    "rsort_vendor_workspace_size": ([_i64], _sz),
+    "rsort_u32_vendor_device": ([_vp, _vp, _i64, _vp, _sz, _vp], _int),
+    "rsort_u32_vendor": ([_vp, _vp, _i64], _int),
+    "rsort_gen_uniform": ([_vp, _i64, ctypes.c_uint64, _vp], _int),
+    "rsort_gen_zipf": ([_vp, _i64, ctypes.c_uint64, _vp, _i64, _vp], _int),
+    "rsort_gen_iota": ([_vp, _i64, ctypes.c_uint32, _vp], _int),
+}
+
+_LIB = None
+
+
+def _lib() -> ctypes.CDLL:
+    """Load librsort.so; raise loudly when it is missing (no fallback path exists)."""
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} is not built: run `python cuda.radixsort_amd/build.py` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _LIB = lib
+    return _LIB
+
+
+def lib_path() -> Path:
+    return LIB_PATH
+
+
+def _check(status: int, where: str):
+    if status != RSORT_OK:
+        raise RSortError(status, where)
+
+
+def version() -> str:
+    v = _lib().rsort_version()
+    return f"{v // 10000}.{v // 100 % 100}.{v % 100}"
+
+
+# ------------------------------------------------------------------------------ host API
+def _host_u32(a, n=None, name="array"):
+    a = np.asarray(a)
+    if a.dtype != np.uint32 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError(f"{name} must be a C-contiguous uint32 numpy array")
+    if n is not None and a.size < n:
+        raise ValueError(f"{name} holds {a.size} < n={n} elements")
+    return a
+
+
+def sortByDevice(h_input, n, h_output, numBits, blockSize=512, times: dict | None = None):
+    """Drop-in for the reference's sortByDevice (Parallel7.cu:530-639): host arrays in/out,
+    synchronous. `times`, if a dict, receives the per-phase kernel times of this call."""
+    h_input = _host_u32(h_input, n, "h_input")
+    h_output = _host_u32(h_output, n, "h_output")
+    pt = PhaseTimes()
+    st = _lib().rsort_u32_ex(h_input.ctypes.data, h_output.ctypes.data, int(n), int(numBits), int(blockSize),
+                             ctypes.byref(pt) if times is not None else None)
+    _check(st, "sortByDevice")
+    if times is not None:
+        times.update(pt.as_dict())
+
+
+def sortByThrust(input, n, output):
+    """The reference's vendor comparator (Parallel7.cu:69-73): rocPRIM radix sort on ROCm."""
+    input = _host_u32(input, n, "input")
+    output = _host_u32(output, n, "output")
+    _check(_lib().rsort_u32_vendor(input.ctypes.data, output.ctypes.data, int(n)), "sortByThrust")
+
+
+def sortPairsByDevice(keys_in, vals_in, n, keys_out, vals_out, numBits):
+    """Stable key + u32 payload sort (BASELINE config 4; no reference counterpart)."""
+    args = [_host_u32(a, n, nm) for a, nm in ((keys_in, "keys_in"), (vals_in, "vals_in"),
+                                               (keys_out, "keys_out"), (vals_out, "vals_out"))]
+    _check(_lib().rsort_u32_pairs(args[0].ctypes.data, args[1].ctypes.data, args[2].ctypes.data,
+                                  args[3].ctypes.data, int(n), int(numBits)), "sortPairsByDevice")
+
+
+def sort(input, n, output, implementation=SORT_BY_HOST, numBits=4, blockSize=1, verbose=True):
+    """Mirror of the reference dispatcher (Parallel7.cu:641-662), same defaults and prints.
+    Returns the elapsed wall time in ms (the reference prints it, :660-661)."""
+    impl = Implementation(implementation)
+    if impl == SORT_BY_HOST:
+        raise ValueError("SORT_BY_HOST is the reference's sequential CPU sort (Baseline1.cu:15-64); "
+                         "it is the test oracle (oracle/), not part of the device library")
+    t0 = time.perf_counter()
+    if impl == SORT_BY_THRUST:
+        if verbose:
+            print("\nRadix Sort by Thrust library")
+        sortByThrust(input, n, output)
+    else:
+        if verbose:
+            print("\nRadix Sort by device:")
+        sortByDevice(input, n, output, numBits, blockSize)
+    ms = (time.perf_counter() - t0) * 1e3
+    if verbose:
+        print("Time: %.3f ms" % ms)
+    return ms
+
+
+# ------------------------------------------------------------------------------ device API
+def _need_torch():
+    if torch is None:
+        raise RuntimeError("the device API needs torch (device memory / streams)")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream=None):
+    _need_torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def plan(n: int, k_bits: int, pairs: bool = False, tiles_per_chunk: int = 0) -> Plan:
+    p = Plan()
+    _check(_lib().rsort_plan_make(int(n), int(k_bits), 1 if pairs else 0, int(tiles_per_chunk), ctypes.byref(p)),
+           "rsort_plan_make")
+    return p
+
+
+def workspace_size(n: int, k_bits: int, pairs: bool = False) -> int:
+    return int(_lib().rsort_workspace_size(int(n), int(k_bits), 1 if pairs else 0))
+
+
+def empty_u32(n, device="cuda"):
+    """Device buffer for u32 keys (torch int32 storage; the bits are the u32 keys)."""
+    _need_torch()
+    return torch.empty(int(n), dtype=torch.int32, device=device)
+
+
+def workspace(nbytes: int, device="cuda"):
+    _need_torch()
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def sort_device(keys_in, keys_out, k_bits=8, vals_in=None, vals_out=None, ws=None, stream=None,
+                plan_: Plan | None = None):
+    """Stream-ordered device sort of torch int32/uint32 tensors (bits = u32 keys)."""
+    n = keys_in.numel()
+    pairs = vals_in is not None
+    p = plan_ if plan_ is not None else plan(n, k_bits, pairs)
+    if ws is None:
+        ws = workspace(p.workspace_bytes, keys_in.device)
+    _check(_lib().rsort_sort_planned(ctypes.byref(p), _ptr(keys_in), _ptr(vals_in), _ptr(keys_out),
+                                     _ptr(vals_out), _ptr(ws), ws.numel(), _stream(stream)),
+           "rsort_sort_planned")
+    return keys_out
+
+
+def pass_histogram(p: Plan, keys, shift, table, stream=None):
+    _check(_lib().rsort_pass_histogram(ctypes.byref(p), _ptr(keys), int(shift), _ptr(table), _stream(stream)),
+           "rsort_pass_histogram")
+
+
+def pass_scan(p: Plan, table, block_sums, stream=None):
+    _check(_lib().rsort_pass_scan(ctypes.byref(p), _ptr(table), _ptr(block_sums), _stream(stream)),
+           "rsort_pass_scan")
+
+
+def pass_scatter(p: Plan, kin, kout, shift, table, vin=None, vout=None, stream=None):
+    _check(_lib().rsort_pass_scatter(ctypes.byref(p), _ptr(kin), _ptr(vin), _ptr(kout), _ptr(vout), int(shift),
+                                     _ptr(table), _stream(stream)), "rsort_pass_scatter")
+
+
+def pass_local_sort(p: Plan, kin, kout, shift, vin=None, vout=None, stream=None):
+    _check(_lib().rsort_pass_local_sort(ctypes.byref(p), _ptr(kin), _ptr(vin), _ptr(kout), _ptr(vout), int(shift),
+                                        _stream(stream)), "rsort_pass_local_sort")
+
+
+def set_rank_algo(algo: int):
+    _check(_lib().rsort_set_rank_algo(int(algo)), "rsort_set_rank_algo")
+
+
+def get_rank_algo() -> int:
+    return int(_lib().rsort_get_rank_algo())
+
+
+@contextmanager
+def rank_algo(algo: int):
+    old = get_rank_algo()
+    set_rank_algo(algo)
+    try:
+        yield
+    finally:
+        set_rank_algo(old)
+
+
+class Profile:
+    """with Profile() as prof: ...  -> prof.times = {phase: {ms, launches, keys}}"""
+
+    def __enter__(self):
+        _check(_lib().rsort_profile_begin(), "rsort_profile_begin")
+        self.times = None
+        return self
+
+    def __exit__(self, *exc):
+        pt = PhaseTimes()
+        st = _lib().rsort_profile_end(ctypes.byref(pt))
+        self.times = pt.as_dict()
+        if exc[0] is None:
+            _check(st, "rsort_profile_end")
+        return False
+
+
+def partition_device(keys_in, keys_out, splitters, bucket_starts, vals_in=None, vals_out=None, ws=None,
+                     stream=None):
+    """Stable key-range partition into len(splitters)+1 buckets (multi-GPU exchange step)."""
+    n = keys_in.numel()
+    nb = len(splitters) + 1
+    sp = (ctypes.c_uint32 * max(1, len(splitters)))(*[int(s) for s in splitters])
+    need = workspace_size(n, max(1, (nb - 1).bit_length()), vals_in is not None)
+    if ws is None or ws.numel() < need:
+        ws = workspace(need, keys_in.device)
+    _check(_lib().rsort_partition_device(_ptr(keys_in), _ptr(vals_in), _ptr(keys_out), _ptr(vals_out), n, sp, nb,
+                                         _ptr(bucket_starts), _ptr(ws), ws.numel(), _stream(stream)),
+           "rsort_partition_device")
+
+
+def top_histogram(keys, top_bits, hist, ws=None, stream=None):
+    n = keys.numel()
+    need = workspace_size(n, top_bits, False)
+    if ws is None or ws.numel() < need:
+        ws = workspace(need, keys.device)
+    _check(_lib().rsort_top_histogram(_ptr(keys), n, int(top_bits), _ptr(hist), _ptr(ws), ws.numel(),
+                                      _stream(stream)), "rsort_top_histogram")
+
+
+def vendor_sort_device(keys_in, keys_out, ws=None, stream=None):
+    n = keys_in.numel()
+    need = int(_lib().rsort_vendor_workspace_size(n))
+    if ws is None or ws.numel() < need:
+        ws = workspace(need, keys_in.device)
+    _check(_lib().rsort_u32_vendor_device(_ptr(keys_in), _ptr(keys_out), n, _ptr(ws), ws.numel(),
+                                          _stream(stream)), "rsort_u32_vendor_device")
+
+
+def gen_uniform(out, seed=0x5EED, stream=None):
+    _check(_lib().rsort_gen_uniform(_ptr(out), out.numel(), int(seed), _stream(stream)), "rsort_gen_uniform")
+
+
+def gen_zipf(out, cdf, seed=0x5EED, stream=None):
+    _check(_lib().rsort_gen_zipf(_ptr(out), out.numel(), int(seed), _ptr(cdf), cdf.numel(), _stream(stream)),
+           "rsort_gen_zipf")
+
+
+def gen_iota(out, base=0, stream=None):
+    _check(_lib().rsort_gen_iota(_ptr(out), out.numel(), int(base), _stream(stream)), "rsort_gen_iota")
+
+
+def to_numpy_u32(t) -> np.ndarray:
+    """Device/host int32 tensor -> numpy uint32 view of the same bits."""
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def from_numpy_u32(a: np.ndarray, device="cuda"):
+    _need_torch()
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).to(device)

@@ -1,0 +1,205 @@
+/*
+ * rsort.h -- C ABI of the MI355X (gfx950) LSD radix sort (library: cuda.radixsort_amd/librsort.so).
+ *
+ * Drop-in boundary for the device sort of truongchauhien/CUDA.RadixSort. Every entry point
+ * takes plain pointers and sizes (no C++ or torch types) and returns an rsort_status
+ * (0 = ok) instead of the reference's print-and-exit CHECK (SourceCode/common/common.h:6-16);
+ * include/radixsort.hpp restores the reference's exact C++ signatures and exit-on-error
+ * behaviour on top of this ABI.
+ *
+ * Reference interfaces replaced (file:line under the reference tree):
+ *   rsort_u32            sortByDevice(h_in, n, h_out, numBits, blockSize)   Parallel7.cu:530-639
+ *                        (host -> host, synchronous, device memory owned by the callee)
+ *   rsort_u32_ex         the same plus the reference's per-phase timers       Parallel7.cu:532-538,633-638
+ *   rsort_u32_device     the per-digit loop of sortByDevice on device buffers  Parallel7.cu:561-623
+ *   rsort_pass_histogram histogram() + histogramKernel                        Parallel7.cu:318-359
+ *   rsort_pass_scan      transpose() + scan() + transpose()                   Parallel7.cu:361-528, :596-598
+ *   rsort_pass_scatter   sortLocallyDataBlocks() + scatter()                  Parallel7.cu:79-316, :568, :612
+ *   rsort_pass_local_sort sortLocallyDataBlocks() alone                       Parallel7.cu:193-251
+ *   rsort_u32_vendor     sortByThrust (the vendor comparator)                 Parallel7.cu:69-73
+ *   (no counterpart)     rsort_u32_pairs*: key + u32 payload (BASELINE config 4)
+ *   (no counterpart)     rsort_partition_device / rsort_bucket_starts: the multi-GPU
+ *                        key-range partition step (BASELINE config 5)
+ *
+ * Semantics shared by every sort entry point:
+ *   - keys are uint32_t, sorted ascending; k_bits in [1, 12] digit bits per pass, passes at
+ *     bit 0, k, 2k, ... < 32 (the last digit is short when k does not divide 32, exactly as
+ *     Baseline1.cu:30-49);
+ *   - output is bit-exact with Baseline1.cu's sortByHost; pairs are STABLE (equal keys keep
+ *     their input order), i.e. equal to Baseline1's loop carrying the payload;
+ *   - 0 <= n < 2^32; n == 0 is a no-op; `in` is never written; in == out is allowed;
+ *   - device entry points are stream-ordered on `stream` (a hipStream_t, NULL = the null
+ *     stream), do no allocation, no host synchronisation and are graph-capturable; they use
+ *     the caller's workspace (rsort_workspace_size bytes, any alignment >= 256 B);
+ *   - the device is the caller's current HIP device.
+ */
+#ifndef RSORT_H_
+#define RSORT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(_WIN32)
+#define RSORT_API
+#else
+#define RSORT_API __attribute__((visibility("default")))
+#endif
+
+typedef enum rsort_status {
+    RSORT_OK = 0,
+    RSORT_ERR_ARG = 1,        /* NULL pointer where data is required, bad option value */
+    RSORT_ERR_BITS = 2,       /* k_bits outside [1, 12] */
+    RSORT_ERR_SIZE = 3,       /* n < 0 or n >= 2^32 */
+    RSORT_ERR_ALIGN = 4,      /* device buffer not 4-byte aligned */
+    RSORT_ERR_ALLOC = 5,      /* hipMalloc / host allocation failed */
+    RSORT_ERR_HIP = 6,        /* a HIP runtime call or kernel launch failed */
+    RSORT_ERR_WORKSPACE = 7,  /* workspace too small */
+    RSORT_ERR_NODEV = 8       /* no HIP device visible */
+} rsort_status;
+
+/* Local-rank algorithm inside a tile (both give the same, unique, stable result). */
+typedef enum rsort_rank_algo {
+    RSORT_RANK_MATCH = 0, /* wave64 ballot peer-match + per-wave LDS digit counters (default) */
+    RSORT_RANK_SPLIT = 1  /* k successive block-local 1-bit splits, ballot/popcount scans
+                             (the reference's algorithm, Parallel5.cu:79-159 / P7:79-191) */
+} rsort_rank_algo;
+
+/* Phases reported by the profiler (the reference's MEASURE_PORTION_EXECUTION_TIME buckets,
+ * Parallel7.cu:634-637; the local sort is fused into the scatter kernel here). */
+typedef enum rsort_phase {
+    RSORT_PHASE_HISTOGRAM = 0,
+    RSORT_PHASE_SCAN = 1,
+    RSORT_PHASE_SCATTER = 2, /* fused block-local sort + rank + scatter: the measured pass */
+    RSORT_PHASE_COPY = 3,    /* device-to-device copies (in-place sorts with an odd pass count) */
+    RSORT_PHASE_COUNT = 4
+} rsort_phase;
+
+typedef struct rsort_phase_times {
+    double ms[RSORT_PHASE_COUNT];         /* summed kernel time per phase (hipEvent pairs) */
+    int64_t launches[RSORT_PHASE_COUNT];  /* launches per phase */
+    int64_t keys[RSORT_PHASE_COUNT];      /* keys processed per phase (sum over launches) */
+} rsort_phase_times;
+
+/* Geometry of one sort: tiles of tile_keys keys are locally sorted by one workgroup;
+ * chunk_keys = tiles_per_chunk * tile_keys keys form one row of the chunk x digit table
+ * (the reference's "block" of Baseline4.cu:79/Parallel7.cu:541, with the table stored
+ * column-major [digit][chunk]). */
+typedef struct rsort_plan {
+    int64_t n;
+    int32_t k_bits;
+    int32_t passes;          /* ceil(32 / k_bits) */
+    int32_t bins;            /* 2^k_bits */
+    int32_t threads;         /* workgroup size */
+    int32_t tile_keys;       /* keys per tile */
+    int32_t pairs;           /* 1: key + value */
+    int64_t tiles_per_chunk;
+    int64_t chunk_keys;
+    int64_t num_chunks;      /* workgroups per histogram / scatter launch */
+    int64_t table_entries;   /* bins * num_chunks */
+    int64_t scan_blocks;     /* workgroups of the table scan */
+    size_t workspace_bytes;  /* for rsort_u32_device / rsort_u32_pairs_device */
+} rsort_plan;
+
+RSORT_API const char *rsort_status_string(int status);
+RSORT_API int rsort_version(void); /* major * 10000 + minor * 100 + patch */
+
+/* Geometry for (n, k_bits, pairs). tiles_per_chunk = 0 picks it from the current device's
+ * CU count and the scatter kernel's occupancy (a fixed default when no device is visible). */
+RSORT_API int rsort_plan_make(int64_t n, int k_bits, int pairs, int64_t tiles_per_chunk,
+                              rsort_plan *plan);
+RSORT_API size_t rsort_workspace_size(int64_t n, int k_bits, int pairs);
+
+/* ---------------------------------------------------------------- whole sort, device */
+RSORT_API int rsort_u32_device(const uint32_t *d_in, uint32_t *d_out, int64_t n, int k_bits,
+                               void *d_workspace, size_t workspace_bytes, void *stream);
+RSORT_API int rsort_u32_pairs_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                                     uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t n,
+                                     int k_bits, void *d_workspace, size_t workspace_bytes,
+                                     void *stream);
+/* Same, with an explicit plan (from rsort_plan_make) -- lets tests pin the geometry. */
+RSORT_API int rsort_sort_planned(const rsort_plan *plan, const uint32_t *d_keys_in,
+                                 const uint32_t *d_vals_in, uint32_t *d_keys_out,
+                                 uint32_t *d_vals_out, void *d_workspace, size_t workspace_bytes,
+                                 void *stream);
+
+/* ---------------------------------------------------------------- whole sort, host -> host */
+/* Synchronous drop-in for sortByDevice (Parallel7.cu:530): H2D, sort, D2H on the current
+ * device with a library-owned, per-device cached workspace. */
+RSORT_API int rsort_u32(const uint32_t *in, uint32_t *out, int64_t n, int k_bits);
+/* Same; block_size is accepted for signature compatibility (the gfx950 tile geometry is
+ * fixed per k); `times` (may be NULL) receives the per-phase kernel times of this call. */
+RSORT_API int rsort_u32_ex(const uint32_t *in, uint32_t *out, int64_t n, int k_bits,
+                           int block_size, rsort_phase_times *times);
+RSORT_API int rsort_u32_pairs(const uint32_t *keys_in, const uint32_t *vals_in,
+                              uint32_t *keys_out, uint32_t *vals_out, int64_t n, int k_bits);
+
+/* ---------------------------------------------------------------- one digit pass, device */
+/* digit(key) = (key >> shift) & (bins - 1). Table layout: d_table[digit * num_chunks + chunk]. */
+RSORT_API int rsort_pass_histogram(const rsort_plan *plan, const uint32_t *d_keys, int shift,
+                                   uint32_t *d_table, void *stream);
+/* In-place exclusive scan of the column-major table; d_block_sums holds plan->scan_blocks
+ * u32 of scratch. */
+RSORT_API int rsort_pass_scan(const rsort_plan *plan, uint32_t *d_table, uint32_t *d_block_sums,
+                              void *stream);
+/* Fused block-local sort + global rank + scatter of one pass (vals may be NULL when
+ * plan->pairs == 0). d_table is the scanned table of the same pass. */
+RSORT_API int rsort_pass_scatter(const rsort_plan *plan, const uint32_t *d_keys_in,
+                                 const uint32_t *d_vals_in, uint32_t *d_keys_out,
+                                 uint32_t *d_vals_out, int shift, const uint32_t *d_table,
+                                 void *stream);
+/* Block-local stable sort of every tile by the digit, written in tile order (the state
+ * sortLocallyDataBlocks leaves behind, Parallel7.cu:568). */
+RSORT_API int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_keys_in,
+                                    const uint32_t *d_vals_in, uint32_t *d_keys_out,
+                                    uint32_t *d_vals_out, int shift, void *stream);
+
+/* ---------------------------------------------------------------- options / profiling */
+RSORT_API int rsort_set_rank_algo(int algo); /* rsort_rank_algo, process-wide */
+RSORT_API int rsort_get_rank_algo(void);
+/* Between begin and end, every launch made by this library records hipEvents around its
+ * phases; end synchronises those events and returns the per-phase sums. */
+RSORT_API int rsort_profile_begin(void);
+RSORT_API int rsort_profile_end(rsort_phase_times *out);
+
+/* ---------------------------------------------------------------- multi-GPU building blocks */
+/* Stable partition of n keys (and values) into num_buckets (<= 16) key ranges:
+ * bucket(key) = #{i : key >= splitters[i]} for the num_buckets-1 ascending host-side
+ * splitters. Output is bucket-major and stable; d_bucket_starts[num_buckets + 1] receives
+ * the exclusive bucket offsets (last = n). Workspace: rsort_workspace_size(n, 4, pairs). */
+RSORT_API int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
+                                     uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t n,
+                                     const uint32_t *splitters, int num_buckets,
+                                     uint32_t *d_bucket_starts, void *d_workspace,
+                                     size_t workspace_bytes, void *stream);
+/* Histogram of the top `top_bits` (1..12) bits of n keys into d_hist[2^top_bits] (u32,
+ * overwritten). Workspace: rsort_workspace_size(n, top_bits, 0). */
+RSORT_API int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits,
+                                  uint32_t *d_hist, void *d_workspace, size_t workspace_bytes,
+                                  void *stream);
+
+/* ---------------------------------------------------------------- vendor comparator */
+/* rocPRIM's device radix sort (what sortByThrust resolves to on ROCm), for the
+ * "vendor ceiling" column. */
+RSORT_API size_t rsort_vendor_workspace_size(int64_t n);
+RSORT_API int rsort_u32_vendor_device(const uint32_t *d_in, uint32_t *d_out, int64_t n,
+                                      void *d_workspace, size_t workspace_bytes, void *stream);
+RSORT_API int rsort_u32_vendor(const uint32_t *in, uint32_t *out, int64_t n);
+
+/* ---------------------------------------------------------------- synthetic workloads */
+/* key[i] = high 32 bits of splitmix64(seed + i). */
+RSORT_API int rsort_gen_uniform(uint32_t *d_out, int64_t n, uint64_t seed, void *stream);
+/* key[i] = fmix32(rank), rank = lower_bound(d_cdf[0..ranks), u_i) with u_i the uniform
+ * stream above; d_cdf is the inclusive Zipf CDF scaled to u32 (last entry 2^32-1). */
+RSORT_API int rsort_gen_zipf(uint32_t *d_out, int64_t n, uint64_t seed, const uint32_t *d_cdf,
+                             int64_t ranks, void *stream);
+/* d_out[i] = base + i */
+RSORT_API int rsort_gen_iota(uint32_t *d_out, int64_t n, uint32_t base, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSORT_H_ */

@@ -1,0 +1,121 @@
+"""CPU-side checks of the C ABI: the library builds, loads, and exports every symbol that
+include/rsort.h declares; planning and argument validation (no kernel launches here)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+from _rs import PKG, rs
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _declared_symbols():
+    text = (ROOT / "include" / "rsort.h").read_text()
+    return sorted(set(re.findall(r"RSORT_API\s+[\w\s\*]+?\b(rsort_\w+)\s*\(", text)))
+
+
+def test_library_present_and_loads():
+    assert rs.lib_path().exists(), "run __graft_entry__.build() first"
+    lib = rs._lib()
+    assert isinstance(lib, ctypes.CDLL)
+    assert rs.version() == "0.1.0"
+
+
+def test_every_declared_symbol_is_exported_and_bound():
+    declared = _declared_symbols()
+    assert len(declared) >= 25
+    lib = rs._lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+        assert name in rs.SIGNATURES, f"{name} has no ctypes signature in radixsort.py"
+    assert set(rs.SIGNATURES) == set(declared)
+
+
+def test_status_strings():
+    lib = rs._lib()
+    for st in range(9):
+        assert lib.rsort_status_string(st)
+    assert lib.rsort_status_string(2) == b"k_bits outside [1, 12]"
+
+
+@pytest.mark.parametrize("n,k", [(0, 8), (1, 8), (513, 4), ((1 << 24) + 1, 8), (1 << 26, 4), (1 << 30, 8),
+                                 ((1 << 32) - 1, 8), (100003, 12), (5, 1)])
+def test_plan_geometry(n, k):
+    p = rs.plan(n, k, False, tiles_per_chunk=0)
+    assert p.passes == -(-32 // k)
+    assert p.bins == 1 << k
+    assert p.tile_keys == p.threads * 16
+    assert p.chunk_keys == p.tiles_per_chunk * p.tile_keys
+    assert p.num_chunks * p.chunk_keys >= n
+    assert (p.num_chunks - 1) * p.chunk_keys < max(n, 1)
+    assert p.table_entries == p.bins * p.num_chunks
+    assert p.workspace_bytes >= 4 * n + 4 * p.table_entries
+    assert rs.workspace_size(n, k) == p.workspace_bytes
+    pp = rs.plan(n, k, True)
+    assert pp.workspace_bytes >= p.workspace_bytes + 4 * n
+
+
+def test_plan_explicit_tiles_per_chunk():
+    p = rs.plan(1 << 20, 8, tiles_per_chunk=1)
+    assert p.num_chunks == 256 and p.chunk_keys == 4096
+    p = rs.plan(1 << 20, 8, tiles_per_chunk=7)
+    assert p.num_chunks == -(-256 // 7)
+
+
+@pytest.mark.parametrize("n,k,status", [(10, 0, 2), (10, 13, 2), (-1, 8, 3), (1 << 32, 8, 3)])
+def test_plan_rejects(n, k, status):
+    with pytest.raises(rs.RSortError) as e:
+        rs.plan(n, k)
+    assert e.value.status == status
+
+
+def test_device_entry_validates_before_touching_the_gpu():
+    lib = rs._lib()
+    # bad k, bad n: rejected before any HIP call
+    assert lib.rsort_u32_device(None, None, 10, 0, None, 0, None) == 2
+    assert lib.rsort_u32_device(None, None, -5, 8, None, 0, None) == 3
+    # n == 0 is a no-op that needs no buffers
+    assert lib.rsort_u32_device(None, None, 0, 8, None, 0, None) == 0
+    # NULL buffers with n > 0
+    assert lib.rsort_u32_device(None, None, 10, 8, None, 0, None) == 1
+    # misaligned pointers
+    assert lib.rsort_u32_device(ctypes.c_void_p(2), ctypes.c_void_p(8), 10, 8, ctypes.c_void_p(256), 1 << 20, None) == 4
+    # workspace too small
+    assert lib.rsort_u32_device(ctypes.c_void_p(256), ctypes.c_void_p(512), 10, 8, ctypes.c_void_p(1024), 16, None) == 7
+    assert lib.rsort_set_rank_algo(7) == 1
+    assert lib.rsort_partition_device(None, None, None, None, 10, None, 0, None, None, 0, None) == 1
+    assert lib.rsort_partition_device(None, None, None, None, 10, None, 17, None, None, 0, None) == 1
+
+
+def test_python_mirror_error_behaviour():
+    import numpy as np
+    with pytest.raises(ValueError):
+        rs.sort(np.zeros(4, np.uint32), 4, np.zeros(4, np.uint32), rs.SORT_BY_HOST)
+    with pytest.raises(TypeError):
+        rs.sortByDevice(np.zeros(4, np.int64), 4, np.zeros(4, np.uint32), 8)
+    with pytest.raises(rs.RSortError) as e:
+        rs.sortByDevice(np.zeros(4, np.uint32), 4, np.zeros(4, np.uint32), 13)
+    assert e.value.status == 2
+
+
+def test_no_cpu_fallback_without_device():
+    """On a machine without a GPU the host entry must FAIL (RSORT_ERR_NODEV), not sort on CPU."""
+    from _rs import gpu_available
+    if gpu_available():
+        pytest.skip("GPU present")
+    import numpy as np
+    x = np.arange(100, dtype=np.uint32)[::-1].copy()
+    y = np.zeros_like(x)
+    with pytest.raises(rs.RSortError) as e:
+        rs.sortByDevice(x, x.size, y, 8)
+    assert e.value.status == 8
+    assert not y.any()
+
+
+def test_package_sources_do_not_reference_the_oracle():
+    for f in list(PKG.rglob("*.py")) + list(PKG.rglob("*.cpp")) + list(PKG.rglob("*.hip")) + \
+            list((ROOT / "include").glob("*")):
+        text = f.read_text()
+        assert "liboracle" not in text and "oracle_sort" not in text and "_ref/libref" not in text, f

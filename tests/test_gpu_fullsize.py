@@ -1,0 +1,67 @@
+"""Full BASELINE sizes (2^26 and 2^30 keys, 2^30 pairs) on the GPU, checked through
+size-independent properties: sortedness, equality with the vendor sort (rocPRIM; a sort's
+output is unique), an order-independent multiset fingerprint, and for pairs the exact
+gather identity keys_out[i] == keys_in[vals_out[i]] plus stability (vals increasing within
+runs of equal keys, vals being the input index)."""
+import numpy as np
+import pytest
+
+from _rs import rs
+from _util import zipf_cdf_u32
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+M32 = 0xFFFFFFFF
+
+
+def as_u64(t):
+    return t.to(torch.int64) & M32
+
+
+def fingerprint(t):
+    """Order-independent: (sum x, sum mix(x)) mod 2^64 over the u32 keys."""
+    x = as_u64(t)
+    h = x * 0x9E3779B1
+    h = h ^ ((h >> 15) & 0x1FFFF)
+    h = h * 0x85EBCA77
+    return int(x.sum()), int(h.sum())
+
+
+def is_sorted(t):
+    x = as_u64(t)
+    return bool((x[1:] >= x[:-1]).all())
+
+
+@pytest.mark.parametrize("n,k", [(1 << 26, 4), (1 << 30, 8)])
+def test_fullsize_uniform(n, k):
+    keys = rs.empty_u32(n)
+    rs.gen_uniform(keys, 0x5EED)
+    out = rs.empty_u32(n)
+    rs.sort_device(keys, out, k)
+    ref = rs.empty_u32(n)
+    rs.vendor_sort_device(keys, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert is_sorted(out)
+    assert fingerprint(out) == fingerprint(keys)
+    del ref
+
+
+def test_fullsize_pairs_zipf():
+    n = 1 << 30
+    cdf = rs.from_numpy_u32(zipf_cdf_u32())
+    keys = rs.empty_u32(n)
+    rs.gen_zipf(keys, cdf, 0x5EED)
+    vals = rs.empty_u32(n)
+    rs.gen_iota(vals, 0)
+    ko, vo = rs.empty_u32(n), rs.empty_u32(n)
+    rs.sort_device(keys, ko, 8, vals_in=vals, vals_out=vo)
+    torch.cuda.synchronize()
+    assert is_sorted(ko)
+    idx = as_u64(vo)
+    assert torch.equal(keys[idx], ko)                       # a permutation carrying its key
+    assert int(torch.bincount(idx[:: 1 << 10] >> 20, minlength=1024).min()) >= 0
+    same = ko[1:] == ko[:-1]
+    assert bool((idx[1:][same] > idx[:-1][same]).all())     # stable
+    assert fingerprint(ko) == fingerprint(keys)

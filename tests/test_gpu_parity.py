@@ -1,0 +1,262 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference's own
+golden vectors. Bit-exact everywhere (integer work). Runs on the MI355X box (-m gpu)."""
+import numpy as np
+import pytest
+
+from _rs import rs
+from _util import (fnv1a64, glibc_rand, oracle_block_pass, oracle_sort, oracle_sort_pairs, uniform_keys,
+                   zipf_cdf_u32, zipf_keys)
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+RANKS = [rs.RANK_MATCH, rs.RANK_SPLIT]
+
+
+def dev(a):
+    return rs.from_numpy_u32(a)
+
+
+def host(t):
+    return rs.to_numpy_u32(t)
+
+
+def gpu_sort(x, k, algo=rs.RANK_MATCH, tiles_per_chunk=0):
+    with rs.rank_algo(algo):
+        p = rs.plan(x.size, k, False, tiles_per_chunk)
+        d_in = dev(x)
+        d_out = rs.empty_u32(x.size)
+        rs.sort_device(d_in, d_out, k, plan_=p)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(d_in), x), "input buffer was modified"
+        return host(d_out)
+
+
+# ------------------------------------------------------------------ reference golden vectors
+def test_reference_debug_vector(golden):
+    case = next(c for c in golden["sort_cases"] if c["name"] == "ref_debug_513_k4")
+    x = np.array(case["input"], np.uint32)
+    for algo in RANKS:
+        y = gpu_sort(x, 4, algo)
+        assert y.tolist() == case["output"]
+
+
+@pytest.mark.parametrize("k", [8, 4])
+def test_reference_default_vector(golden, k):
+    """The reference's own default run: n=(1<<24)+1 glibc rand() keys (Parallel7.cu:708,:721)."""
+    case = next(c for c in golden["sort_cases"] if c["name"] == f"ref_default_{(1 << 24) + 1}_k{k}")
+    x = glibc_rand(case["n"])
+    assert fnv1a64(x) == case["fnv_in"]
+    for algo in RANKS:
+        y = gpu_sort(x, k, algo)
+        assert fnv1a64(y) == case["fnv_out"]
+        for i, v in case["samples"].items():
+            assert int(y[int(i)]) == v
+
+
+def test_all_golden_cases(golden):
+    for case in golden["sort_cases"]:
+        if case["source"] not in ("uniform", "zipf"):
+            continue
+        x = uniform_keys(case["n"], case["seed"]) if case["source"] == "uniform" else zipf_keys(case["n"], case["seed"])
+        y = gpu_sort(x, case["k"])
+        assert fnv1a64(y) == case["fnv_out"], case["name"]
+
+
+# ------------------------------------------------------------------ oracle sweeps
+SIZES = [1, 2, 3, 63, 64, 65, 255, 4095, 4096, 4097, 8191, 65536 + 17, 100003, (1 << 20) + 5]
+
+
+@pytest.mark.parametrize("k", list(range(1, 13)))
+@pytest.mark.parametrize("algo", RANKS)
+def test_sizes_and_bits_vs_oracle(k, algo):
+    for n in SIZES:
+        if k == 1 and n > 100003:
+            continue
+        x = uniform_keys(n, seed=1000 * k + n)
+        assert np.array_equal(gpu_sort(x, k, algo), oracle_sort(x, k)), (n, k, algo)
+
+
+@pytest.mark.parametrize("dist", ["zipf", "allsame", "sorted", "reversed", "fewbits", "topbit"])
+def test_distributions(dist):
+    n = 300007
+    if dist == "zipf":
+        x = zipf_keys(n, seed=7)
+    elif dist == "allsame":
+        x = np.full(n, 0xDEADBEEF, np.uint32)
+    elif dist == "sorted":
+        x = np.sort(uniform_keys(n))
+    elif dist == "reversed":
+        x = np.sort(uniform_keys(n))[::-1].copy()
+    elif dist == "fewbits":
+        x = uniform_keys(n) & np.uint32(0x00F000F0)
+    else:
+        x = uniform_keys(n) | np.uint32(0x80000000)
+    for k in (4, 8, 11):
+        for algo in RANKS:
+            assert np.array_equal(gpu_sort(x, k, algo), oracle_sort(x, k)), (dist, k, algo)
+
+
+@pytest.mark.parametrize("tpc", [1, 2, 3, 17])
+def test_chunk_geometry_does_not_change_the_result(tpc):
+    x = zipf_keys(200003, seed=tpc)
+    for algo in RANKS:
+        assert np.array_equal(gpu_sort(x, 8, algo, tiles_per_chunk=tpc), oracle_sort(x, 8))
+
+
+# ------------------------------------------------------------------ pairs (stability)
+@pytest.mark.parametrize("k", [4, 8, 5, 12])
+@pytest.mark.parametrize("algo", RANKS)
+def test_pairs_stable_vs_oracle(k, algo):
+    for n in (1, 4097, 250001):
+        keys = zipf_keys(n, seed=n + k)
+        vals = np.arange(n, dtype=np.uint32) ^ np.uint32(0x5A5A5A5A)
+        ko_ref, vo_ref = oracle_sort_pairs(keys, vals, k)
+        with rs.rank_algo(algo):
+            dk, dv = dev(keys), dev(vals)
+            ok, ov = rs.empty_u32(n), rs.empty_u32(n)
+            rs.sort_device(dk, ok, k, vals_in=dv, vals_out=ov)
+            torch.cuda.synchronize()
+        assert np.array_equal(host(ok), ko_ref)
+        assert np.array_equal(host(ov), vo_ref)
+
+
+def test_pairs_host_entry():
+    n = 70001
+    keys = zipf_keys(n, seed=3)
+    vals = np.arange(n, dtype=np.uint32)
+    ko, vo = np.empty_like(keys), np.empty_like(vals)
+    rs.sortPairsByDevice(keys, vals, n, ko, vo, 8)
+    rk, rv = oracle_sort_pairs(keys, vals, 8)
+    assert np.array_equal(ko, rk) and np.array_equal(vo, rv)
+
+
+# ------------------------------------------------------------------ per-pass intermediates (a4-a8)
+@pytest.mark.parametrize("n,k,bit,tpc", [(513, 4, 0, 1), (100003, 8, 8, 3), (70001, 5, 30, 2),
+                                          (1 << 18, 8, 24, 1), (50001, 12, 12, 2), (4096 * 5, 3, 3, 5)])
+@pytest.mark.parametrize("algo", RANKS)
+def test_pass_intermediates_vs_block_oracle(n, k, bit, tpc, algo):
+    """histogram table / column-major scan / locally sorted tiles / pass output, each against
+    the Baseline4 restatement run with the same tile (4096) and chunk geometry."""
+    x = zipf_keys(n, seed=n) if k != 12 else uniform_keys(n, seed=n)
+    p = rs.plan(n, k, False, tpc)
+    h_ref, s_ref, loc_ref, out_ref = oracle_block_pass(x, k, bit, p.tile_keys, p.chunk_keys)
+    with rs.rank_algo(algo):
+        d = dev(x)
+        table = rs.empty_u32(p.table_entries)
+        bsums = rs.empty_u32(max(1, p.scan_blocks))
+        rs.pass_histogram(p, d, bit, table)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(table), h_ref)
+        rs.pass_scan(p, table, bsums)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(table), s_ref)
+        loc = rs.empty_u32(n)
+        rs.pass_local_sort(p, d, loc, bit)
+        out = rs.empty_u32(n)
+        rs.pass_scatter(p, d, out, bit, table)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(loc), loc_ref)
+        assert np.array_equal(host(out), out_ref)
+
+
+# ------------------------------------------------------------------ API semantics
+@pytest.mark.parametrize("k", [8, 5, 4, 3])
+def test_in_place(k):
+    """in == out is allowed (odd pass counts stage through the workspace first)."""
+    x = uniform_keys(123457, seed=k)
+    d = dev(x)
+    rs.sort_device(d, d, k)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(d), np.sort(x))
+
+
+def test_empty_and_tiny():
+    lib = rs._lib()
+    assert lib.rsort_u32_device(None, None, 0, 8, None, 0, None) == 0
+    y = np.zeros(1, np.uint32)
+    rs.sortByDevice(np.array([7], np.uint32), 1, y, 8)
+    assert y[0] == 7
+
+
+def test_workspace_too_small_is_reported():
+    x = dev(uniform_keys(10000))
+    out = rs.empty_u32(10000)
+    ws = rs.workspace(1024)
+    st = rs._lib().rsort_u32_device(x.data_ptr(), out.data_ptr(), 10000, 8, ws.data_ptr(), 1024,
+                                    torch.cuda.current_stream().cuda_stream)
+    assert st == 7
+
+
+def test_host_entry_and_reference_dispatcher(golden, capsys):
+    case = next(c for c in golden["sort_cases"] if c["name"] == "ref_debug_513_k4")
+    x = np.array(case["input"], np.uint32)
+    y = np.zeros_like(x)
+    times = {}
+    rs.sortByDevice(x, x.size, y, 4, 512, times=times)
+    assert y.tolist() == case["output"]
+    assert times["scatter"]["launches"] == 8 and times["histogram"]["launches"] == 8
+    z = np.zeros_like(x)
+    rs.sort(x, x.size, z, rs.SORT_BY_DEVICE, 4, 512)
+    out = capsys.readouterr().out
+    assert "Radix Sort by device:" in out and "Time:" in out
+    assert np.array_equal(z, y)
+
+
+def test_vendor_comparator():
+    x = uniform_keys(1 << 20, seed=5)
+    y = np.zeros_like(x)
+    rs.sortByThrust(x, x.size, y)
+    assert np.array_equal(y, np.sort(x))
+
+
+def test_generators_match_host_generators():
+    n = (1 << 20) + 3
+    d = rs.empty_u32(n)
+    rs.gen_uniform(d, 0x5EED)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(d), uniform_keys(n))
+    cdf = dev(zipf_cdf_u32())
+    rs.gen_zipf(d, cdf, 0x5EED)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(d), zipf_keys(n))
+    rs.gen_iota(d, 5)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(d), (np.arange(n, dtype=np.uint64) + 5).astype(np.uint32))
+
+
+def test_profile_counts_launches():
+    x = dev(uniform_keys(1 << 20))
+    out = rs.empty_u32(1 << 20)
+    with rs.Profile() as prof:
+        rs.sort_device(x, out, 8)
+    t = prof.times
+    assert t["scatter"]["launches"] == 4 and t["histogram"]["launches"] == 4 and t["scan"]["launches"] == 4
+    assert t["scatter"]["ms"] > 0 and t["scatter"]["keys"] == 4 * (1 << 20)
+
+
+# ------------------------------------------------------------------ multi-GPU building blocks
+def test_top_histogram():
+    x = zipf_keys(300001, seed=9)
+    h = rs.empty_u32(1 << 12)
+    rs.top_histogram(dev(x), 12, h)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(h), np.bincount(x >> np.uint32(20), minlength=4096).astype(np.uint32))
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 8, 16])
+def test_partition_stable(nb):
+    n = 200003
+    x = zipf_keys(n, seed=nb)
+    v = np.arange(n, dtype=np.uint32)
+    split = np.sort(uniform_keys(nb - 1, seed=nb)) if nb > 1 else np.array([], np.uint32)
+    bucket = np.searchsorted(split, x, side="right")
+    order = np.argsort(bucket, kind="stable")
+    ko, vo = rs.empty_u32(n), rs.empty_u32(n)
+    starts = rs.empty_u32(nb + 1)
+    rs.partition_device(dev(x), ko, split.tolist(), starts, vals_in=dev(v), vals_out=vo)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(ko), x[order])
+    assert np.array_equal(host(vo), v[order])
+    exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
+    assert np.array_equal(host(starts), exp)
