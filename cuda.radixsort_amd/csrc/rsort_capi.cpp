@@ -82,42 +82,52 @@ int hip_status(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP
 bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
 
 // ------------------------------------------------------------------------------ planning
-int device_shape(int bits, int pairs, int *cus, int *bpc) {
-    *cus = 256;
-    *bpc = 4;
-    int dev = 0, count = 0;
+int device_cus() {
+    int dev = 0, count = 0, c = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
-        *cus = c;
-    const int b = scatter_blocks_per_cu(bits, pairs, g_rank_algo.load());
-    if (b > 0) *bpc = b;
-    return 1;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return c;
 }
 
-int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p) {
+// Tile geometry for one sort: long digit runs (16384-key tiles) for k = 5..8, 8192-key tiles
+// for k <= 4 keys, 4096-key tiles otherwise -- and 4096-key tiles whenever the input is too
+// small to give every CU two large tiles.
+int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
+    if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
+    const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
+    if (k >= 5 && k <= 8 && n >= enough * geom_tile_keys(kGeomLarge)) return kGeomLarge;
+    if (k <= 4 && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
+    return kGeomSmall;
+}
+
+int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int partition = 0) {
     if (!p) return RSORT_ERR_ARG;
     if (k < kMinBits || k > kMaxBits) return RSORT_ERR_BITS;
     if (n < 0 || n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
     if (tpc < 0) return RSORT_ERR_ARG;
     memset(p, 0, sizeof(*p));
+    const int rank = g_rank_algo.load();
+    const int cus = device_cus();
+    const int geom = choose_geom(n, k, pairs, rank, partition, cus);
+    const int tile = geom_tile_keys(geom);
     p->n = n;
     p->k_bits = k;
     p->passes = (32 + k - 1) / k;
     p->bins = 1 << k;
-    p->threads = kThreads;
-    p->tile_keys = kTileKeys;
+    p->threads = kGeomShape[geom].threads;
+    p->tile_keys = tile;
     p->pairs = pairs ? 1 : 0;
-    const int64_t tiles = std::max<int64_t>(1, (n + kTileKeys - 1) / kTileKeys);
+    const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
     if (tpc == 0) {
-        int cus, bpc;
-        device_shape(k, pairs, &cus, &bpc);
-        const int64_t target = std::max<int64_t>(1, (int64_t)cus * bpc);
+        // one resident wave of workgroups: as many chunks as the scatter kernel keeps resident
+        int bpc = cus > 0 ? scatter_blocks_per_cu(k, pairs, partition ? RSORT_RANK_MATCH : rank, geom) : 0;
+        if (bpc <= 0) bpc = 2;
+        const int64_t target = std::max<int64_t>(1, (int64_t)(cus > 0 ? cus : 256) * bpc);
         tpc = (tiles + target - 1) / target;
     }
     p->tiles_per_chunk = tpc;
-    p->chunk_keys = tpc * kTileKeys;
+    p->chunk_keys = tpc * tile;
     p->num_chunks = (tiles + tpc - 1) / tpc;
     p->table_entries = (int64_t)p->bins * p->num_chunks;
     p->scan_blocks = (p->table_entries + kScanSegment - 1) / kScanSegment;
@@ -195,17 +205,20 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     a.nsplit = (uint32_t)nsplit;
     for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
     const int rank = (dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH;
+    const int geom = geom_from_shape(p.threads, p.tile_keys);
+    if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
-    return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, a, s));
+    return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, a, s));
 }
 
 int check_plan(const rsort_plan *p) {
     if (!p) return RSORT_ERR_ARG;
     if (p->k_bits < kMinBits || p->k_bits > kMaxBits) return RSORT_ERR_BITS;
     if (p->n < 0 || p->n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (geom_from_shape(p->threads, p->tile_keys) < 0) return RSORT_ERR_ARG;
     if (p->tiles_per_chunk <= 0 || p->num_chunks <= 0 ||
-        p->num_chunks * p->tiles_per_chunk * kTileKeys < p->n ||
-        p->chunk_keys != p->tiles_per_chunk * kTileKeys || p->bins != (1 << p->k_bits) ||
+        p->num_chunks * p->tiles_per_chunk * p->tile_keys < p->n ||
+        p->chunk_keys != p->tiles_per_chunk * p->tile_keys || p->bins != (1 << p->k_bits) ||
         p->table_entries != (int64_t)p->bins * p->num_chunks)
         return RSORT_ERR_ARG;
     return RSORT_OK;
@@ -501,6 +514,15 @@ int rsort_profile_end(rsort_phase_times *out) {
     return st;
 }
 
+size_t rsort_partition_workspace_size(int64_t n, int num_buckets, int pairs) {
+    if (num_buckets < 1 || num_buckets > kMaxSplitters + 1) return 0;
+    int bits = 1;
+    while ((1 << bits) < num_buckets) ++bits;
+    rsort_plan p;
+    if (plan_fill(n, bits, pairs, 0, &p, /*partition=*/1) != RSORT_OK) return 0;
+    return p.workspace_bytes;
+}
+
 int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in, uint32_t *d_keys_out,
                            uint32_t *d_vals_out, int64_t n, const uint32_t *splitters, int num_buckets,
                            uint32_t *d_bucket_starts, void *d_workspace, size_t workspace_bytes,
@@ -513,7 +535,7 @@ int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
     while ((1 << bits) < num_buckets) ++bits;
     const int pairs = d_vals_in != nullptr;
     rsort_plan p;
-    int st = plan_fill(n, bits, pairs, 0, &p);
+    int st = plan_fill(n, bits, pairs, 0, &p, /*partition=*/1);
     if (st) return st;
     if (!d_bucket_starts) return RSORT_ERR_ARG;
     hipStream_t s = (hipStream_t)stream;

@@ -7,9 +7,7 @@
 namespace rsort {
 
 constexpr int kWave = 64;
-constexpr int kThreads = 256;              // workgroup size of every pass kernel
-constexpr int kKeysPerThread = 16;         // keys per thread per tile
-constexpr int kTileKeys = kThreads * kKeysPerThread;  // 4096 keys = 16 KiB per tile
+constexpr int kHistThreads = 256;          // workgroup size of the histogram kernel
 constexpr int kMinBits = 1;
 constexpr int kMaxBits = 12;
 constexpr int kScanThreads = 256;
@@ -18,6 +16,23 @@ constexpr int kScanSegment = kScanThreads * kScanPerThread;  // table entries pe
 constexpr int kMaxSplitters = 15;          // partition: <= 16 buckets
 
 enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
+
+// Scatter-kernel tile geometries (threads x keys per thread). Measured on MI355X at 2^30 keys
+// (dev/scatter_lab): the digit runs a tile writes must be long enough to fill 128-B lines, so
+// k = 5..8 uses 16384-key tiles; k <= 4 has long runs already; k >= 9 and small inputs use
+// 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
+enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomCount = 3 };
+struct GeomShape {
+    int threads;
+    int kpt;
+};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}};
+inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
+inline int geom_from_shape(int threads, int tile_keys) {
+    for (int g = 0; g < kGeomCount; ++g)
+        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) return g;
+    return -1;
+}
 
 struct HistArgs {
     const uint32_t *keys;
@@ -44,6 +59,7 @@ struct ScatterArgs {
     uint32_t local_only;    // 1: write each tile's local order back in place of the tile
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
+    unsigned long long *stamps;  // diagnostic builds (RSORT_STAMPS) only: per-phase cycles
 };
 
 struct ScanArgs {
@@ -55,8 +71,10 @@ struct ScanArgs {
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.
 hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t s);
-hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, const ScatterArgs &a,
-                          hipStream_t s);
+hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom,
+                          const ScatterArgs &a, hipStream_t s);
+// Whether a (bits, pairs, rank_algo, dmode, geom) scatter kernel is compiled in.
+bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom);
 hipError_t launch_scan(const ScanArgs &a, hipStream_t s);
 hipError_t launch_gather_starts(const uint32_t *table, uint32_t num_chunks, uint32_t bins,
                                 uint64_t n, uint32_t *starts, hipStream_t s);
@@ -67,6 +85,6 @@ hipError_t launch_gen_zipf(uint32_t *out, uint64_t n, uint64_t seed, const uint3
                            uint64_t ranks, hipStream_t s);
 hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t s);
 // Resident scatter workgroups per CU (occupancy query), 0 on error.
-int scatter_blocks_per_cu(int bits, int pairs, int rank_algo);
+int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom);
 
 }  // namespace rsort

@@ -31,22 +31,64 @@
 
 #include "rsort_internal.hpp"
 
+// Diagnostic phase stamps (dev/scatter_lab only; compiled out of the library): wave 0 of each
+// workgroup accumulates s_memtime deltas per phase of the scatter tile loop.
+#ifdef RSORT_STAMPS
+#define RS_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define RS_STAMP(i)                                                   \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[i] += now_ - st_prev;                                  \
+        st_prev = now_;                                               \
+    } while (0)
+#define RS_STAMP_WAIT_LOADS() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#define RS_STAMP_FLUSH()                                                          \
+    do {                                                                          \
+        if (threadIdx.x == 0 && a.stamps)                                         \
+            for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 8 + i_] = st_acc[i_]; \
+    } while (0)
+#else
+#define RS_STAMP_DECL
+#define RS_STAMP(i)
+#define RS_STAMP_WAIT_LOADS()
+#define RS_STAMP_FLUSH()
+#endif
+
 namespace rsort {
 
-enum RankAlgo : int { kRankMatch = 0, kRankSplit = 1 };
+enum RankAlgo : int { kRankMatch = 0, kRankSplit = 1, kRankMatchRW = 2, kRankCount = 3 };
 
 // ------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-    const uint32_t l = lane_id();
+// Mask (lo, hi halves) of the lanes of this wave whose BITS-bit digit equals this lane's:
+// AND over bits b of (ballot(bit b) XNOR my bit b), one v_bitop3 per half per bit
+// (truth table 0x90 = a & ~(b ^ c) with a = mask, b = ballot half, c = my bit as 0 / ~0).
+template <int BITS>
+__device__ __forceinline__ void peer_mask(uint32_t d, uint32_t &mlo, uint32_t &mhi) {
+    mlo = ~0u;
+    mhi = ~0u;
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, kWave);
-        if (l >= (uint32_t)o) x += y;
+    for (int b = 0; b < BITS; ++b) {
+        int s = __builtin_amdgcn_sbfe((int)d, b, 1);
+        asm volatile("" : "+v"(s));  // keep s opaque: the ballot then compares s itself (1 VALU)
+        const uint64_t bal = __ballot(s);
+        mlo = __builtin_amdgcn_bitop3_b32(mlo, (uint32_t)bal, (uint32_t)s, 0x90);
+        mhi = __builtin_amdgcn_bitop3_b32(mhi, (uint32_t)(bal >> 32), (uint32_t)s, 0x90);
     }
+}
+
+// Inclusive wave64 scan with DPP row shifts + row broadcasts (no LDS, no bpermute):
+// row_shr:1,2,4,8 scan each row of 16 lanes, row_bcast:15 / row_bcast:31 carry row totals.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
 }
 
@@ -188,21 +230,55 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 // write each digit's run to global at table[digit][chunk] + (earlier tiles' count) +
 // (position - first position of the digit in the tile) -- the firstIndices rank formula of
 // P7:293-294 with the running offset kept in registers.
-template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE>
-__global__ __launch_bounds__(THREADS) void rs_scatter(ScatterArgs a) {
+//
+// The next tile's keys are loaded into registers as soon as the current tile is staged in
+// LDS, so its HBM reads overlap the current tile's global writes.
+//
+// Template knobs (the library picks one configuration per (BITS, PAIRS); dev/scatter_lab
+// times the others):
+//   RANK  kRankMatch   leader lane bumps the per-wave digit counter with a returning ds_add,
+//                      the base is broadcast with ds_bpermute (slots never wait on each other)
+//         kRankMatchRW all lanes read the counter, the leader writes it back (no broadcast;
+//                      one LDS round trip per slot on the wave's critical path)
+//         kRankCount   count first (one non-returning ds_add per key), scan the per-wave
+//                      counters into final tile positions, then peer-match each slot and write
+//                      the key straight to its LDS position: no per-key rank registers and no
+//                      separate staging loop (lowest VGPR use -> most workgroups per CU)
+//         kRankSplit   k stable 1-bit splits (the reference's algorithm)
+//   DEST  stage each key's global destination next to it in LDS (keys only): the output
+//         phase then reads (key, destination) with two conflict-free reads, no dependent lookup
+//   MINW  minimum waves per SIMD requested from the register allocator (0 = compiler's choice)
+//   ABL   ablation bits for dev/scatter_lab only (1 = skip ranking, 2 = skip global stores)
+template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW = 0,
+          bool DEST = false, int ABL = 0, bool WC = false>
+__global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(ScatterArgs a) {
+    static_assert(!(DEST && PAIRS), "DEST staging is for keys-only sorts");
+    static_assert(!WC || (RANK == kRankCount && (1u << BITS) <= (uint32_t)THREADS),
+                  "write-combining needs the count-first ranking and one digit per thread");
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;            // tile positions per wave
     constexpr uint32_t T = THREADS * KPT;       // tile keys
     constexpr int DPT = (R > THREADS) ? (int)(R / THREADS) : 1;  // digits owned per thread
-    constexpr uint32_t NCNT = (RANK == kRankMatch) ? W * R : R;
+    constexpr bool MATCH = (RANK == kRankMatch || RANK == kRankMatchRW);
+    static_assert(RANK != kRankCount || !DEST, "kRankCount writes keys during ranking");
+    constexpr uint32_t NCNT = (MATCH || RANK == kRankCount) ? W * R : R;
 
     __shared__ uint32_t s_keys[T];
     __shared__ uint32_t s_vals[PAIRS ? T : 1];
+    __shared__ uint32_t s_dest[DEST ? T : 1];
     __shared__ uint16_t s_aux[RANK == kRankSplit ? T : 1];
     __shared__ uint32_t s_cnt[NCNT];
-    __shared__ uint32_t s_delta[R];
+    __shared__ uint32_t s_delta[WC ? 1 : R];
     __shared__ uint32_t s_ws[W];
+    // write-combining state (WC): per-digit carry of <= 31 keys that did not fill a 128-B line,
+    // its count | invalid-prefix << 8, the new-carry copy spec, and the tile's line records
+    // {global line start, tile source start, digit, carry count | invalid-prefix << 8}
+    __shared__ uint32_t s_carry[WC ? R * 32 : 1];
+    __shared__ uint32_t s_cvals[WC && PAIRS ? R * 32 : 1];
+    __shared__ uint32_t s_cc[WC ? R : 1];
+    __shared__ uint32_t s_nc[WC ? R : 1];
+    __shared__ uint4 s_line[WC ? T / 32 + R : 1];
 
     const uint32_t t = threadIdx.x;
     const uint32_t w = t / kWave;
@@ -222,51 +298,271 @@ __global__ __launch_bounds__(THREADS) void rs_scatter(ScatterArgs a) {
     }
 
     const uint32_t base = w * SEG + lane;
-    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+    // Tile loader: positions past the end read as 0xFFFFFFFF, whose digit is the largest
+    // possible one, so they rank after every real key of the tile and are never written out.
+    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        uint32_t key[KPT];
-        uint32_t val[PAIRS ? KPT : 1];
-        uint32_t dg[KPT];
-        // ---- load (positions past the end become digit R-1, which sorts them last)
+        // wave-uniform tile base + 32-bit lane offsets: saddr loads with immediate offsets, no
+        // per-slot 64-bit address registers kept alive across the tile loop
+        const uint32_t *__restrict__ tk = a.kin + tb;
+        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb : nullptr;
         if (valid == T) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                key[j] = a.kin[tb + base + j * kWave];
-                if constexpr (PAIRS) val[j] = a.vin[tb + base + j * kWave];
+                k[j] = tk[base + j * kWave];
+                if constexpr (PAIRS) v[j] = tv[base + j * kWave];
             }
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) dg[j] = dig(key[j]);
         } else {
+            // lane-relative limit: slot j is real iff j*64 < lim (no per-slot offset registers)
+            const uint32_t lim = valid > base ? valid - base : 0u;
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                const uint32_t p = base + j * kWave;
-                key[j] = p < valid ? a.kin[tb + p] : 0xFFFFFFFFu;
-                if constexpr (PAIRS) val[j] = p < valid ? a.vin[tb + p] : 0u;
-                dg[j] = p < valid ? dig(key[j]) : R - 1;
+                const bool in = (uint32_t)(j * kWave) < lim;
+                k[j] = in ? tk[base + j * kWave] : 0xFFFFFFFFu;
+                if constexpr (PAIRS) v[j] = in ? tv[base + j * kWave] : 0u;
             }
         }
-        for (uint32_t i = t; i < NCNT; i += THREADS) s_cnt[i] = 0;
-        __syncthreads();
+    };
 
-        uint32_t rk[KPT];
-        if constexpr (RANK == kRankMatch) {
-            // ---- wave peer-match ranking; counters s_cnt[w][digit]
-            const uint64_t below = lanes_below();
+    uint32_t key[KPT];
+    uint32_t val[PAIRS ? KPT : 1];
+    if (cbeg < cend) load_tile(cbeg, key, val);
+    if constexpr (WC) {
+        // the chunk's first line of each digit starts (run & 31) keys early: those slots belong to
+        // the previous chunk and are marked invalid (never written by this workgroup)
+        if (t < R && !a.local_only) s_cc[t] = (run[0] & 31u) * 0x101u;
+    }
+
+    RS_STAMP_DECL
+    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        // output slot j of thread t (LDS position t + j*THREADS) is real iff j*THREADS < olim;
+        // comparing constants against one register keeps LICM from hoisting KPT positions
+        // tl: the thread index made opaque per tile, so LICM cannot hoist the KPT output
+        // positions tl + j*THREADS out of the loop into KPT live registers
+        uint32_t tl = t;
+        asm volatile("" : "+v"(tl));
+        const uint32_t olim = valid > tl ? valid - tl : 0u;
+        const uint64_t nb = tb + T;
+        RS_STAMP_WAIT_LOADS();
+        RS_STAMP(0);  // waiting for this tile's keys (and the previous tile's stores)
+
+        if constexpr (RANK != kRankCount) {
+            for (uint32_t i = t; i < NCNT; i += THREADS) s_cnt[i] = 0;
+            __syncthreads();
+        }
+        RS_STAMP(1);  // counter reset + barrier
+
+        if constexpr (RANK == kRankCount) {
+            // ---- 0. each wave clears its own counters: no other wave touches s_cnt[w][*]
+            //      between the previous tile's digit scan (behind two barriers) and this point
+#pragma unroll
+            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+            // ---- 1. per-wave digit histogram of the tile
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+            __syncthreads();
+            RS_STAMP(2);  // histogram
+            // ---- 2. digit scan: s_cnt[w][d] <- tile position of wave w's first key of digit d.
+            // With WC, each digit's output is cut into whole 128-B lines: its previous-tile carry
+            // (c keys, line-aligned start A = g - c) + this tile's run, minus the new tail carry.
+            // One packed scan yields both the digit starts (low 16 bits) and line offsets (high).
+            uint32_t tot[DPT];
+            uint32_t mine = 0;
+#pragma unroll
+            for (int i = 0; i < DPT; ++i) {
+                const uint32_t d = t * DPT + i;
+                uint32_t acc = 0;
+                if (d < R) {
+#pragma unroll
+                    for (int v = 0; v < W; ++v) {
+                        const uint32_t x = s_cnt[v * R + d];
+                        s_cnt[v * R + d] = acc;
+                        acc += x;
+                    }
+                }
+                tot[i] = acc;
+                mine += acc;
+            }
+            uint32_t wc_A = 0, wc_c = 0, wc_inv = 0, wc_nfull = 0, wc_leff = 0, wc_ccn = 0;
+            if constexpr (WC) {
+                if (t < R) {
+                    const uint32_t d = t;
+                    // padding (last tile only) has the largest digit and sits at its run's end
+                    wc_leff = tot[0];
+                    if (valid < T && d == dig(0xFFFFFFFFu)) wc_leff -= T - valid;
+                    const uint32_t cc = s_cc[d];
+                    wc_c = cc & 0xFFu;
+                    wc_inv = cc >> 8;
+                    const uint32_t g = run[0];
+                    wc_A = g - wc_c;
+                    const uint32_t e = g + wc_leff;
+                    const uint32_t fe = e & ~31u;
+                    wc_nfull = fe > wc_A ? (fe - wc_A) >> 5 : 0u;
+                    mine |= wc_nfull << 16;
+                }
+            }
+            uint32_t all;
+            const uint32_t pstart = block_excl_scan<THREADS>(mine, s_ws, all);
+            uint32_t start = WC ? (pstart & 0xFFFFu) : pstart;
+#pragma unroll
+            for (int i = 0; i < DPT; ++i) {
+                const uint32_t d = t * DPT + i;
+                if (d < R) {
+#pragma unroll
+                    for (int v = 0; v < W; ++v) s_cnt[v * R + d] += start;
+                    if constexpr (WC) {
+                        const uint32_t lo = pstart >> 16;
+                        for (uint32_t k = 0; k < wc_nfull; ++k)
+                            s_line[lo + k] = make_uint4(wc_A + 32u * k, start - wc_c + 32u * k, d,
+                                                        k == 0 ? (wc_c | (wc_inv << 8)) : 0u);
+                        // the new tail carry: what is left of carry + run after the whole lines
+                        const uint32_t e = run[i] + wc_leff;
+                        uint32_t cnew, inew;
+                        if (wc_nfull > 0) {
+                            cnew = e & 31u;
+                            inew = 0;
+                            s_nc[d] = (start + wc_leff - cnew) | (cnew << 24);
+                        } else {
+                            cnew = wc_c + wc_leff;
+                            inew = wc_inv;
+                            s_nc[d] = start | (wc_c << 16) | (wc_leff << 24);
+                        }
+                        wc_ccn = cnew | (inew << 8);
+                        run[i] = e;
+                    } else {
+                        s_delta[d] = run[i] - start;
+                        run[i] += tot[i];
+                    }
+                }
+                start += tot[i];
+            }
+            __syncthreads();
+            RS_STAMP(3);  // barrier + digit scan
+            // ---- 3. peer-match each slot; the counter IS the destination: write the key now
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                uint64_t m = ~0ull;
-#pragma unroll
-                for (int b = 0; b < BITS; ++b) {
-                    const uint32_t bit = (dg[j] >> b) & 1u;
-                    const uint64_t bal = __ballot(bit);
-                    m &= bit ? bal : ~bal;
-                }
-                const uint32_t pre = (uint32_t)__popcll(m & below);
-                uint32_t old = 0;
-                if (pre == 0) old = atomicAdd(&s_cnt[w * R + dg[j]], (uint32_t)__popcll(m));
-                old = __shfl(old, (int)__ffsll((unsigned long long)m) - 1, kWave);
-                rk[j] = old + pre;
+                // recompute the digit: CSE with the histogram step would keep KPT addresses alive
+                asm volatile("" : "+v"(key[j]));
+                const uint32_t d = dig(key[j]);
+                uint32_t mlo, mhi;
+                peer_mask<BITS>(d, mlo, mhi);
+                const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                const uint32_t old = s_cnt[w * R + d];
+                if (pre == 0) s_cnt[w * R + d] = old + (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi));
+                s_keys[old + pre] = key[j];
+                if constexpr (PAIRS) s_vals[old + pre] = val[j];
             }
+            __syncthreads();
+            RS_STAMP(4);  // ranking + staging + barrier
+            if (nb < cend) load_tile(nb, key, val);
+            if (a.local_only) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = tl + j * THREADS;
+                    if ((uint32_t)(j * THREADS) < olim) {
+                        a.kout[tb + i] = s_keys[i];
+                        if constexpr (PAIRS) a.vout[tb + i] = s_vals[i];
+                    }
+                }
+            } else if constexpr (WC) {
+                // ---- 4. whole aligned lines only: 32 lanes per 128-B line, 2 lines per wave store
+                const uint32_t nl = all >> 16;
+#pragma unroll 8
+                for (uint32_t item = tl; item < nl * 32u; item += THREADS) {
+                    const uint4 rec = s_line[item >> 5];
+                    const uint32_t q = item & 31u;
+                    const bool from_carry = q < (rec.w & 0xFFu);
+                    const uint32_t k = from_carry ? s_carry[rec.z * 32u + q] : s_keys[rec.y + q];
+                    uint32_t v = 0;
+                    if constexpr (PAIRS) v = from_carry ? s_cvals[rec.z * 32u + q] : s_vals[rec.y + q];
+                    if constexpr ((ABL & 2) != 0) {
+                        asm volatile("" ::"v"(k), "v"(v));
+                        continue;
+                    }
+                    if (q >= (rec.w >> 8)) {  // first line of a chunk: slots below belong to the previous chunk
+                        a.kout[rec.x + q] = k;
+                        if constexpr (PAIRS) a.vout[rec.x + q] = v;
+                    }
+                }
+                __syncthreads();  // every old carry has been read
+                // ---- 5. save the new tail carries (<= 31 keys per digit)
+#pragma unroll 8
+                for (uint32_t item = tl; item < R * 32u; item += THREADS) {
+                    const uint32_t d = item >> 5, x = item & 31u;
+                    const uint32_t nc = s_nc[d];
+                    if (x < (nc >> 24)) {
+                        const uint32_t dst = d * 32u + ((nc >> 16) & 0xFFu) + x;
+                        s_carry[dst] = s_keys[(nc & 0xFFFFu) + x];
+                        if constexpr (PAIRS) s_cvals[dst] = s_vals[(nc & 0xFFFFu) + x];
+                    }
+                }
+                if (t < R) s_cc[t] = wc_ccn;
+            } else {
+                const bool full = valid == T;
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = tl + j * THREADS;
+                    if (full || (uint32_t)(j * THREADS) < olim) {
+                        const uint32_t k = s_keys[i];
+                        const uint32_t pos = s_delta[dig(k)] + i;
+                        if constexpr ((ABL & 2) != 0) {
+                            asm volatile("" ::"v"(k), "v"(pos));
+                            continue;
+                        }
+                        a.kout[pos] = k;
+                        if constexpr (PAIRS) a.vout[pos] = s_vals[i];
+                    }
+                    // issue the output in groups of 8 keys: bounds the LDS reads in flight
+                    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            RS_STAMP(5);  // output: LDS reads + global stores issued
+        } else if constexpr (MATCH) {
+            // ---- wave peer-match ranking; counters s_cnt[w][digit]. Per slot: the mask of
+            // lanes holding the same digit (BITS ballots, 4 VALU per bit), the rank among them
+            // (mbcnt), and the per-wave digit counter bumped once per digit group.
+            uint32_t rk[KPT];    // rank of the key inside its wave (counter base + rank in group)
+            uint32_t info[KPT];  // digit | (kRankMatch: rank in group << 16 | leader lane << 24)
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = dig(key[j]);  // padding 0xFFFFFFFF -> the largest digit
+                if constexpr ((ABL & 1) != 0) {
+                    rk[j] = (uint32_t)j * kWave + lane;
+                    info[j] = d;
+                    continue;
+                }
+                uint32_t mlo, mhi;
+                peer_mask<BITS>(d, mlo, mhi);
+                const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                const uint32_t cnt = (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi));
+                if constexpr (RANK == kRankMatch) {
+                    // returning ds_add by the group's lowest lane; broadcast in the second loop
+                    const uint32_t leader = mlo ? (uint32_t)__builtin_ctz(mlo) : 32u + (uint32_t)__builtin_ctz(mhi);
+                    rk[j] = 0;
+                    if (pre == 0) rk[j] = atomicAdd(&s_cnt[w * R + d], cnt);
+                    info[j] = d | (pre << 16) | (leader << 24);
+                    // Materialise the packed state now: otherwise the compiler sinks the leader
+                    // computation to its use and keeps all KPT 64-bit masks alive (~+40 VGPRs).
+                    asm volatile("" : "+v"(info[j]));
+                } else {
+                    // every lane reads the counter (same address within a group: broadcast), the
+                    // group's lowest lane writes it back; in-order LDS keeps slots consistent
+                    const uint32_t old = s_cnt[w * R + d];
+                    if (pre == 0) s_cnt[w * R + d] = old + cnt;
+                    rk[j] = (old + pre) | (d << 16);  // wave rank < 64*KPT, digit < 2^12: one register
+                    asm volatile("" : "+v"(rk[j]));   // materialise now (else old/pre/d stay live per slot)
+                    info[j] = 0;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one slot's temporaries at a time
+            }
+            if constexpr (RANK == kRankMatch && (ABL & 1) == 0) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j)
+                    rk[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((info[j] >> 24) << 2), (int)rk[j]) +
+                            ((info[j] >> 16) & 0xFFu);
+            }
+            RS_STAMP(2);  // ranking
             __syncthreads();
             // ---- digit scan: per owned digit, exclusive over waves; block scan over digits
             uint32_t tot[DPT];
@@ -300,38 +596,63 @@ __global__ __launch_bounds__(THREADS) void rs_scatter(ScatterArgs a) {
                 start += tot[i];
             }
             __syncthreads();
-            // ---- stage the tile in digit order
+            RS_STAMP(3);  // barrier + digit scan
+            // ---- stage the tile in digit order (and, with DEST, each key's global position)
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                const uint32_t pos = s_cnt[w * R + dg[j]] + rk[j];
+                uint32_t d, r;
+                if constexpr (RANK == kRankMatchRW && (ABL & 1) == 0) {
+                    d = rk[j] >> 16;
+                    r = rk[j] & 0xFFFFu;
+                } else {
+                    d = info[j] & 0xFFFFu;
+                    r = rk[j];
+                }
+                const uint32_t pos = s_cnt[w * R + d] + r;
                 s_keys[pos] = key[j];
                 if constexpr (PAIRS) s_vals[pos] = val[j];
+                if constexpr (DEST) s_dest[pos] = s_delta[d] + pos;
             }
             __syncthreads();
+            RS_STAMP(4);  // staging + barrier
+            if (nb < cend) load_tile(nb, key, val);
             // ---- write each digit's run: consecutive threads -> consecutive addresses
             if (a.local_only) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = t + j * THREADS;
-                    if (i < valid) {
+                    const uint32_t i = tl + j * THREADS;
+                    if ((uint32_t)(j * THREADS) < olim) {
                         a.kout[tb + i] = s_keys[i];
                         if constexpr (PAIRS) a.vout[tb + i] = s_vals[i];
                     }
                 }
             } else {
+                const bool full = valid == T;
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = t + j * THREADS;
-                    if (i < valid) {
+                    const uint32_t i = tl + j * THREADS;
+                    if (full || (uint32_t)(j * THREADS) < olim) {
                         const uint32_t k = s_keys[i];
-                        const uint32_t pos = s_delta[dig(k)] + i;
+                        uint32_t pos;
+                        if constexpr (DEST) pos = s_dest[i];
+                        else pos = s_delta[dig(k)] + i;
+                        if constexpr ((ABL & 2) != 0) {
+                            asm volatile("" ::"v"(k), "v"(pos));
+                            continue;
+                        }
+                        // ranks are fake under ABL & 1: keep the ablation's stores inside the buffer
+                        if constexpr ((ABL & 1) != 0) pos = (uint32_t)((uint64_t)pos % a.n);
                         a.kout[pos] = k;
                         if constexpr (PAIRS) a.vout[pos] = s_vals[i];
                     }
                 }
             }
+            RS_STAMP(5);  // output: LDS reads + global stores issued
         } else {
             // ---- RANK_SPLIT: k stable 1-bit splits in LDS (reference P5:89-146 / P7:79-191)
+            uint32_t dg[KPT];
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) dg[j] = dig(key[j]);  // padding 0xFFFFFFFF -> the largest digit
             const uint64_t below = lanes_below();
 #pragma unroll 1
             for (int b = 0; b < BITS; ++b) {
@@ -404,8 +725,28 @@ __global__ __launch_bounds__(THREADS) void rs_scatter(ScatterArgs a) {
                     if constexpr (PAIRS) a.vout[pos] = val[j];
                 }
             }
+            if (nb < cend) load_tile(nb, key, val);
         }
     }
+    if constexpr (WC) {
+        if (!a.local_only) {
+            // ---- chunk end: flush every digit's tail carry (a partial line shared with the next chunk)
+            __syncthreads();                    // the last tile's carry copy is complete
+            if (t < R) s_nc[t] = run[0];        // end of this chunk's output for digit t
+            __syncthreads();
+            for (uint32_t item = t; item < R * 32u; item += THREADS) {
+                const uint32_t d = item >> 5, x = item & 31u;
+                const uint32_t cc = s_cc[d];
+                const uint32_t c = cc & 0xFFu;
+                if (x < c && x >= (cc >> 8)) {
+                    const uint32_t gpos = s_nc[d] - c + x;
+                    a.kout[gpos] = s_carry[d * 32u + x];
+                    if constexpr (PAIRS) a.vout[gpos] = s_cvals[d * 32u + x];
+                }
+            }
+        }
+    }
+    RS_STAMP_FLUSH();
 }
 
 // ------------------------------------------------------------------------------ small kernels
@@ -470,50 +811,66 @@ template <int BITS>
 static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
-            rs_histogram<BITS, kThreads, kDigitSplit><<<a.num_chunks, kThreads, 0, s>>>(a);
+            rs_histogram<BITS, kHistThreads, kDigitSplit><<<a.num_chunks, kHistThreads, 0, s>>>(a);
             return hipGetLastError();
         }
         return hipErrorInvalidValue;
     }
-    rs_histogram<BITS, kThreads, kDigitShift><<<a.num_chunks, kThreads, 0, s>>>(a);
+    rs_histogram<BITS, kHistThreads, kDigitShift><<<a.num_chunks, kHistThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
-template <int BITS, bool PAIRS, int RANK, int DMODE>
+// The compiled scatter kernels. "match" (the default rank algorithm) is the count-first peer
+// match (kRankCount); "split" is the reference's 1-bit split sort. Geometries per kGeomShape.
+template <int BITS, bool PAIRS, int RANK, int DMODE, int G>
 static void *scatter_fn() {
-    return reinterpret_cast<void *>(&rs_scatter<BITS, kThreads, kKeysPerThread, PAIRS, RANK, DMODE>);
+    constexpr int TH = kGeomShape[G].threads;
+    constexpr int KPT = kGeomShape[G].kpt;
+    constexpr int MINW = (G == kGeomK4) ? 4 : 0;
+    return reinterpret_cast<void *>(&rs_scatter<BITS, TH, KPT, PAIRS, RANK, DMODE, MINW>);
 }
 
-template <int BITS>
-static void *scatter_pick(int pairs, int rank, int dmode) {
+template <int BITS, bool PAIRS>
+static void *scatter_pick2(int rank, int dmode, int geom) {
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
-            return pairs ? scatter_fn<BITS, true, kRankMatch, kDigitSplit>()
-                         : scatter_fn<BITS, false, kRankMatch, kDigitSplit>();
+            if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankCount, kDigitSplit, kGeomSmall>();
         }
         return nullptr;
     }
-    if (rank == kRankSplit)
-        return pairs ? scatter_fn<BITS, true, kRankSplit, kDigitShift>()
-                     : scatter_fn<BITS, false, kRankSplit, kDigitShift>();
-    return pairs ? scatter_fn<BITS, true, kRankMatch, kDigitShift>()
-                 : scatter_fn<BITS, false, kRankMatch, kDigitShift>();
+    if (rank == kRankSplit) {
+        if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankSplit, kDigitShift, kGeomSmall>();
+        return nullptr;
+    }
+    if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomSmall>();
+    if constexpr (BITS >= 5 && BITS <= 8) {
+        if (geom == kGeomLarge) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomLarge>();
+    }
+    if constexpr (BITS <= 4 && !PAIRS) {
+        if (geom == kGeomK4) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomK4>();
+    }
+    return nullptr;
 }
 
-static void *scatter_kernel(int bits, int pairs, int rank, int dmode) {
+template <int BITS>
+static void *scatter_pick(int pairs, int rank, int dmode, int geom) {
+    return pairs ? scatter_pick2<BITS, true>(rank, dmode, geom) : scatter_pick2<BITS, false>(rank, dmode, geom);
+}
+
+static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom) {
     switch (bits) {
-        case 1: return scatter_pick<1>(pairs, rank, dmode);
-        case 2: return scatter_pick<2>(pairs, rank, dmode);
-        case 3: return scatter_pick<3>(pairs, rank, dmode);
-        case 4: return scatter_pick<4>(pairs, rank, dmode);
-        case 5: return scatter_pick<5>(pairs, rank, dmode);
-        case 6: return scatter_pick<6>(pairs, rank, dmode);
-        case 7: return scatter_pick<7>(pairs, rank, dmode);
-        case 8: return scatter_pick<8>(pairs, rank, dmode);
-        case 9: return scatter_pick<9>(pairs, rank, dmode);
-        case 10: return scatter_pick<10>(pairs, rank, dmode);
-        case 11: return scatter_pick<11>(pairs, rank, dmode);
-        case 12: return scatter_pick<12>(pairs, rank, dmode);
+        case 1: return scatter_pick<1>(pairs, rank, dmode, geom);
+        case 2: return scatter_pick<2>(pairs, rank, dmode, geom);
+        case 3: return scatter_pick<3>(pairs, rank, dmode, geom);
+        case 4: return scatter_pick<4>(pairs, rank, dmode, geom);
+        case 5: return scatter_pick<5>(pairs, rank, dmode, geom);
+        case 6: return scatter_pick<6>(pairs, rank, dmode, geom);
+        case 7: return scatter_pick<7>(pairs, rank, dmode, geom);
+        case 8: return scatter_pick<8>(pairs, rank, dmode, geom);
+        case 9: return scatter_pick<9>(pairs, rank, dmode, geom);
+        case 10: return scatter_pick<10>(pairs, rank, dmode, geom);
+        case 11: return scatter_pick<11>(pairs, rank, dmode, geom);
+        case 12: return scatter_pick<12>(pairs, rank, dmode, geom);
         default: return nullptr;
     }
 }
@@ -536,20 +893,28 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
     }
 }
 
-hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, const ScatterArgs &a,
-                          hipStream_t s) {
-    void *fn = scatter_kernel(bits, pairs, rank_algo, dmode);
+bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom) {
+    if (geom < 0 || geom >= kGeomCount) return false;
+    return scatter_kernel(bits, pairs, rank_algo, dmode, geom) != nullptr;
+}
+
+hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom,
+                          const ScatterArgs &a, hipStream_t s) {
+    if (geom < 0 || geom >= kGeomCount) return hipErrorInvalidValue;
+    void *fn = scatter_kernel(bits, pairs, rank_algo, dmode, geom);
     if (!fn) return hipErrorInvalidValue;
     ScatterArgs copy = a;
     void *args[] = {&copy};
-    return hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kThreads), args, 0, s);
+    return hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
 }
 
-int scatter_blocks_per_cu(int bits, int pairs, int rank_algo) {
-    void *fn = scatter_kernel(bits, pairs, rank_algo, kDigitShift);
+int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom) {
+    if (geom < 0 || geom >= kGeomCount) return 0;
+    void *fn = scatter_kernel(bits, pairs, rank_algo, kDigitShift, geom);
     if (!fn) return 0;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kThreads, 0) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kGeomShape[geom].threads, 0) != hipSuccess)
+        return 0;
     return nb;
 }
 

@@ -50,9 +50,8 @@ class GpuOps:
         ko = torch.empty_like(keys)
         vo = torch.empty_like(vals) if vals is not None else None
         starts = torch.empty(nb + 1, dtype=torch.int32, device=self.device)
-        bits = max(1, (nb - 1).bit_length())
-        rs.partition_device(keys, ko, splitters, starts, vals_in=vals, vals_out=vo,
-                            ws=self._workspace(rs.workspace_size(n, bits, vals is not None)))
+        need = int(rs._lib().rsort_partition_workspace_size(n, nb, 1 if vals is not None else 0))
+        rs.partition_device(keys, ko, splitters, starts, vals_in=vals, vals_out=vo, ws=self._workspace(need))
         return ko, vo, starts
 
     def sort(self, keys, vals, k_bits, out_keys=None, out_vals=None):

@@ -103,6 +103,7 @@ SIGNATURES = {
     "rsort_get_rank_algo": ([], _int),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
+    "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
     "rsort_partition_device": ([_vp, _vp, _vp, _vp, _i64, _u32p, _int, _vp, _vp, _sz, _vp], _int),
     "rsort_top_histogram": ([_vp, _i64, _int, _vp, _vp, _sz, _vp], _int),
     "rsort_vendor_workspace_size": ([_i64], _sz),
@@ -319,7 +320,7 @@ def partition_device(keys_in, keys_out, splitters, bucket_starts, vals_in=None, 
     n = keys_in.numel()
     nb = len(splitters) + 1
     sp = (ctypes.c_uint32 * max(1, len(splitters)))(*[int(s) for s in splitters])
-    need = workspace_size(n, max(1, (nb - 1).bit_length()), vals_in is not None)
+    need = int(_lib().rsort_partition_workspace_size(n, nb, 1 if vals_in is not None else 0))
     if ws is None or ws.numel() < need:
         ws = workspace(need, keys_in.device)
     _check(_lib().rsort_partition_device(_ptr(keys_in), _ptr(vals_in), _ptr(keys_out), _ptr(vals_out), n, sp, nb,

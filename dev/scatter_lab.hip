@@ -1,0 +1,190 @@
+// scatter_lab.hip -- development harness (not part of the library): times variants of the
+// fused local-sort + scatter kernel and HBM ceilings on the current GPU, and checks every
+// variant's pass output against the first variant's (the pass output is unique).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc \
+//         dev/scatter_lab.hip -o dev/scatter_lab && dev/scatter_lab [log2n]
+#include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+using namespace rsort;
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            printf("HIP error %s at line %d\n", hipGetErrorString(e_), __LINE__);          \
+            exit(1);                                                                       \
+        }                                                                                  \
+    } while (0)
+
+__global__ void count_mismatch(const uint32_t *a, const uint32_t *b, uint64_t n, unsigned long long *bad) {
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        local += a[i] != b[i];
+    if (local) atomicAdd(bad, local);
+}
+
+__global__ void copy_dword(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+__global__ void copy_dwordx4(const uint4 *__restrict__ in, uint4 *__restrict__ out, uint64_t n4) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+struct Ctx {
+    uint64_t n;
+    uint32_t *keys, *vals, *out, *vout, *ref, *table, *bsums;
+    unsigned long long *bad;
+    unsigned long long *stamps;
+    int cus;
+    hipEvent_t e0, e1;
+    bool have_ref = false;
+};
+
+template <typename F>
+float time_ms(Ctx &c, int reps, F f) {
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(c.e0, 0));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(c.e1, 0));
+    CK(hipEventSynchronize(c.e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, c.e0, c.e1));
+    return ms / reps;
+}
+
+static const char *g_filter = nullptr;
+
+template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int MINW, bool DEST = false, int ABL = 0,
+          bool WC = false>
+void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
+    if (g_filter && !strstr(name, g_filter)) return;
+    auto kern = rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, kDigitShift, MINW, DEST, ABL, WC>;
+    int bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, THREADS, 0));
+    const uint64_t T = (uint64_t)THREADS * KPT;
+    const uint64_t tiles = (c.n + T - 1) / T;
+    const uint64_t target = (uint64_t)(c.cus * bpc * wave_mult);
+    const uint64_t tpc = (tiles + target - 1) / target;
+    const uint64_t chunks = (tiles + tpc - 1) / tpc;
+    HistArgs h{};
+    h.keys = c.keys;
+    h.table = c.table;
+    h.n = c.n;
+    h.chunk_keys = tpc * T;
+    h.num_chunks = (uint32_t)chunks;
+    h.shift = shift;
+    h.vec = 1;
+    CK(launch_histogram(BITS, kDigitShift, h, 0));
+    ScanArgs s{};
+    s.table = c.table;
+    s.block_sums = c.bsums;
+    s.m = (uint64_t)chunks << BITS;
+    s.nblocks = (uint32_t)((s.m + kScanSegment - 1) / kScanSegment);
+    CK(launch_scan(s, 0));
+    ScatterArgs a{};
+    a.kin = c.keys;
+    a.vin = c.vals;
+    a.kout = c.out;
+    a.vout = c.vout;
+    a.table = c.table;
+    a.n = c.n;
+    a.chunk_keys = tpc * T;
+    a.num_chunks = (uint32_t)chunks;
+    a.shift = shift;
+    a.stamps = c.stamps;
+    CK(hipMemset(c.out, 0, c.n * 4));
+    const float ms = time_ms(c, reps, [&] { kern<<<chunks, THREADS>>>(a); });
+    CK(hipGetLastError());
+    unsigned long long bad = 0;
+    if (!c.have_ref) {
+        CK(hipMemcpy(c.ref, c.out, c.n * 4, hipMemcpyDeviceToDevice));
+        c.have_ref = true;
+    } else {
+        CK(hipMemset(c.bad, 0, 8));
+        count_mismatch<<<4096, 256>>>(c.out, c.ref, c.n, c.bad);
+        CK(hipMemcpy(&bad, c.bad, 8, hipMemcpyDeviceToHost));
+    }
+    const double bytes = (PAIRS ? 16.0 : 8.0) * c.n;
+    printf("%-34s bpc=%d tpc=%-5llu chunks=%-6llu %8.3f ms  %7.1f GB/s  %5.1f%%  mismatch=%llu\n", name, bpc,
+           (unsigned long long)tpc, (unsigned long long)chunks, ms, bytes / ms / 1e6, bytes / ms / 1e6 / 80.0, bad);
+#ifdef RSORT_STAMPS
+    {
+        std::vector<unsigned long long> st(chunks * 8);
+        CK(hipMemcpy(st.data(), c.stamps, chunks * 8 * 8, hipMemcpyDeviceToHost));
+        double sum[8] = {0}, tot = 0;
+        for (uint64_t b = 0; b < chunks; ++b)
+            for (int i = 0; i < 8; ++i) sum[i] += st[b * 8 + i];
+        for (int i = 0; i < 8; ++i) tot += sum[i];
+        const char *names[8] = {"wait-keys", "reset+bar", "rank", "scan", "stage", "output", "-", "-"};
+        printf("    stamps per tile (cycles, wave 0):");
+        for (int i = 0; i < 6; ++i) printf(" %s=%.0f (%.0f%%)", names[i], sum[i] / chunks / tpc, 100.0 * sum[i] / tot);
+        printf("\n");
+    }
+#endif
+    fflush(stdout);
+}
+
+int main(int argc, char **argv) {
+    Ctx c{};
+    const int lg = argc > 1 ? atoi(argv[1]) : 30;
+    g_filter = argc > 2 ? argv[2] : nullptr;
+    c.n = (1ull << lg) - (argc > 3 ? strtoull(argv[3], nullptr, 10) : 0ull);
+    CK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
+    CK(hipMalloc(&c.keys, c.n * 4));
+    CK(hipMalloc(&c.vals, c.n * 4));
+    CK(hipMalloc(&c.out, c.n * 4));
+    CK(hipMalloc(&c.vout, c.n * 4));
+    CK(hipMalloc(&c.ref, c.n * 4));
+    CK(hipMalloc(&c.table, (c.n / 1024 + 65536) * 4 * 16));
+    CK(hipMalloc(&c.bsums, 1 << 24));
+    CK(hipMalloc(&c.bad, 8));
+    CK(hipMalloc(&c.stamps, 65536 * 8 * 8));
+    CK(hipEventCreate(&c.e0));
+    CK(hipEventCreate(&c.e1));
+    CK(launch_gen_uniform(c.keys, c.n, 0x5EED, 0));
+    CK(launch_gen_iota(c.vals, c.n, 0, 0));
+    CK(hipDeviceSynchronize());
+    printf("n=%llu cus=%d\n", (unsigned long long)c.n, c.cus);
+
+    if (!g_filter) {
+        const float ms1 = time_ms(c, 5, [&] { copy_dword<<<c.cus * 8, 256>>>(c.keys, c.out, c.n); });
+        const float ms4 = time_ms(c, 5, [&] { copy_dwordx4<<<c.cus * 8, 256>>>((const uint4 *)c.keys, (uint4 *)c.out, c.n / 4); });
+        const float ms4b = time_ms(c, 5, [&] { copy_dwordx4<<<c.cus * 32, 256>>>((const uint4 *)c.keys, (uint4 *)c.out, c.n / 4); });
+        printf("copy dword   %8.3f ms %7.1f GB/s\n", ms1, 8.0 * c.n / ms1 / 1e6);
+        printf("copy dwordx4 %8.3f ms %7.1f GB/s\n", ms4, 8.0 * c.n / ms4 / 1e6);
+        printf("copy dwordx4 (32/CU) %8.3f ms %7.1f GB/s\n", ms4b, 8.0 * c.n / ms4b / 1e6);
+    }
+    constexpr int M = kRankMatch;
+    constexpr int RW = kRankMatchRW;
+    constexpr int CT = kRankCount;
+    variant<8, 256, 16, false, M, 0>(c, "k8 256x16 match (ref)", 1.0);
+    variant<8, 256, 16, false, CT, 0>(c, "k8 256x16 count", 1.0);
+    variant<8, 256, 32, false, CT, 0>(c, "k8 256x32 count", 1.0);
+    variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count", 1.0);
+    variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count x2", 2.0);
+    variant<8, 256, 64, false, CT, 0>(c, "k8 256x64 count", 1.0);
+    variant<8, 1024, 16, false, CT, 0>(c, "k8 1024x16 count", 1.0);
+    c.have_ref = false;
+    variant<8, 256, 16, true, M, 0>(c, "k8 pairs 256x16 match (ref)", 1.0);
+    variant<8, 512, 16, true, RW, 0>(c, "k8 pairs 512x16 matchRW", 1.0);
+    variant<8, 256, 32, true, RW, 0>(c, "k8 pairs 256x32 matchRW", 1.0);
+    variant<8, 512, 16, true, CT, 0>(c, "k8 pairs 512x16 count", 1.0);
+    variant<8, 512, 32, true, CT, 0>(c, "k8 pairs 512x32 count", 1.0);
+    c.have_ref = false;
+    variant<4, 256, 16, false, M, 0>(c, "k4 256x16 match (ref)", 1.0);
+    variant<4, 256, 16, false, CT, 0>(c, "k4 256x16 count", 1.0);
+    variant<4, 512, 16, false, CT, 4>(c, "k4 512x16 count w4", 1.0);
+    variant<4, 512, 32, false, CT, 0>(c, "k4 512x32 count", 1.0);
+    return 0;
+}

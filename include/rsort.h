@@ -169,7 +169,8 @@ RSORT_API int rsort_profile_end(rsort_phase_times *out);
 /* Stable partition of n keys (and values) into num_buckets (<= 16) key ranges:
  * bucket(key) = #{i : key >= splitters[i]} for the num_buckets-1 ascending host-side
  * splitters. Output is bucket-major and stable; d_bucket_starts[num_buckets + 1] receives
- * the exclusive bucket offsets (last = n). Workspace: rsort_workspace_size(n, 4, pairs). */
+ * the exclusive bucket offsets (last = n). Workspace: rsort_partition_workspace_size. */
+RSORT_API size_t rsort_partition_workspace_size(int64_t n, int num_buckets, int pairs);
 RSORT_API int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
                                      uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t n,
                                      const uint32_t *splitters, int num_buckets,

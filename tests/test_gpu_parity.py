@@ -97,6 +97,24 @@ def test_distributions(dist):
             assert np.array_equal(gpu_sort(x, k, algo), oracle_sort(x, k)), (dist, k, algo)
 
 
+@pytest.mark.parametrize("k", [8, 6, 5, 4, 3])
+def test_large_tile_geometries(k):
+    """n >= 2 * CUs * tile selects the 16384-key (k = 5..8) / 8192-key (k <= 4) tiles; ragged
+    tails and zipf keys, keys and pairs, against the oracle."""
+    n = (1 << 23) + 12345
+    keys = zipf_keys(n, seed=k) if k % 2 else uniform_keys(n, seed=k)
+    p = rs.plan(n, k, False)
+    assert p.tile_keys in (8192, 16384), p.as_dict()
+    assert np.array_equal(gpu_sort(keys, k), oracle_sort(keys, k))
+    if k >= 5:
+        vals = np.arange(n, dtype=np.uint32)
+        ko, vo = rs.empty_u32(n), rs.empty_u32(n)
+        rs.sort_device(dev(keys), ko, k, vals_in=dev(vals), vals_out=vo)
+        torch.cuda.synchronize()
+        rk, rv = oracle_sort_pairs(keys, vals, k)
+        assert np.array_equal(host(ko), rk) and np.array_equal(host(vo), rv)
+
+
 @pytest.mark.parametrize("tpc", [1, 2, 3, 17])
 def test_chunk_geometry_does_not_change_the_result(tpc):
     x = zipf_keys(200003, seed=tpc)
