@@ -63,5 +63,23 @@ def build(force: bool = False) -> Path:
     return LIB
 
 
+CLI_SRC = ROOT / "tools" / "rsort_cli.cpp"
+CLI = ROOT / "tools" / "rsort_cli"
+
+
+def build_cli(force: bool = False) -> Path:
+    """The reference-harness CLI (tools/rsort_cli.cpp), linked against librsort.so."""
+    lib = build(force)
+    if force or _stale(CLI, [CLI_SRC, lib, ROOT / "include" / "radixsort.hpp"]):
+        cmd = [HIPCC, "-O2", "-std=c++17", f"-I{ROOT / 'include'}", str(CLI_SRC), "-o", str(CLI),
+               f"-L{PKG}", "-lrsort", "-Wl,-rpath,$ORIGIN/../cuda.radixsort_amd"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError("build of tools/rsort_cli failed")
+    return CLI
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))
+    print(build_cli())

@@ -1,0 +1,78 @@
+// radixsort.hpp -- the reference's C++ sort interface, served by the MI355X library.
+//
+// Drop-in for SourceCode/Parallel*.cu of truongchauhien/CUDA.RadixSort: a file that defined
+//     typedef enum {SORT_BY_HOST, SORT_BY_THRUST, SORT_BY_DEVICE} Implementation;   (P7:22)
+//     void sortByThrust(const uint32_t *in, int n, uint32_t *out);                 (P7:69-73)
+//     void sortByDevice(const uint32_t *h_in, int n, uint32_t *h_out,
+//                       int numBits, int blockSize);                               (P7:530-639)
+//     void sort(const uint32_t *in, int n, uint32_t *out,
+//               Implementation = SORT_BY_HOST, int numBits = 4, int blockSize = 1); (P7:641-662)
+// deletes those definitions (and its __global__ kernels), keeps its own sortByHost and main,
+// includes this header and links librsort.so. Names, argument order (in, n, out, ...),
+// default arguments, stdout lines and exit-on-error behaviour are the reference's:
+//   - "\nRadix Sort by device:\n" / "\nRadix Sort by Thrust library\n" / "\nRadix Sort by host\n"
+//     and "Time: %.3f ms\n" (P7:650-661); with RSORT_MEASURE_PORTION_EXECUTION_TIME defined,
+//     the per-phase lines of P7:633-638 ("Sort locally blocks" is fused into "Scatter" here);
+//   - any failure prints "Error: file:line, code: c, reason: r" to stderr and exits with
+//     EXIT_FAILURE, as the reference's CHECK does (common/common.h:6-16).
+// SORT_BY_HOST dispatches to the caller's sortByHost, exactly as the reference's sort() does;
+// this library provides no host sort and never falls back to one.
+#pragma once
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <chrono>
+
+#include "rsort.h"
+
+typedef enum { SORT_BY_HOST, SORT_BY_THRUST, SORT_BY_DEVICE } Implementation;
+
+// Provided by the caller, as in every reference source file (Baseline1.cu:15-64).
+void sortByHost(const uint32_t *in, int n, uint32_t *out, int nBits);
+
+namespace radixsort_compat {
+inline void check(int status, const char *file, int line) {
+    if (status != RSORT_OK) {
+        fprintf(stderr, "Error: %s:%d, ", file, line);
+        fprintf(stderr, "code: %d, reason: %s\n", status, rsort_status_string(status));
+        exit(EXIT_FAILURE);
+    }
+}
+}  // namespace radixsort_compat
+
+#define RSORT_CHECK(call) radixsort_compat::check((call), __FILE__, __LINE__)
+
+inline void sortByThrust(const uint32_t *in, int n, uint32_t *out) {
+    RSORT_CHECK(rsort_u32_vendor(in, out, (int64_t)n));
+}
+
+inline void sortByDevice(const uint32_t *h_input, int n, uint32_t *h_output, int numBits,
+                         int blockSize) {
+    rsort_phase_times t;
+    RSORT_CHECK(rsort_u32_ex(h_input, h_output, (int64_t)n, numBits, blockSize, &t));
+#ifdef RSORT_MEASURE_PORTION_EXECUTION_TIME
+    printf(">>>> Time | Sort locally blocks   : %.3f\n", 0.0);
+    printf(">>>> Time | Histogram             : %.3f\n", t.ms[RSORT_PHASE_HISTOGRAM]);
+    printf(">>>> Time | Scan                  : %.3f\n", t.ms[RSORT_PHASE_SCAN]);
+    printf(">>>> Time | Scatter               : %.3f\n", t.ms[RSORT_PHASE_SCATTER]);
+#endif
+}
+
+inline void sort(const uint32_t *in, int n, uint32_t *out, Implementation implementation = SORT_BY_HOST,
+                 int numBits = 4, int blockSize = 1) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (implementation == SORT_BY_HOST) {
+        printf("\nRadix Sort by host\n");
+        sortByHost(in, n, out, numBits);
+    } else if (implementation == SORT_BY_THRUST) {
+        printf("\nRadix Sort by Thrust library\n");
+        sortByThrust(in, n, out);
+    } else {
+        printf("\nRadix Sort by device:\n");
+        sortByDevice(in, n, out, numBits, blockSize);
+    }
+    const std::chrono::duration<double, std::milli> dt = std::chrono::steady_clock::now() - t0;
+    printf("Time: %.3f ms\n", dt.count());
+}

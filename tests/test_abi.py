@@ -121,3 +121,36 @@ def test_package_sources_do_not_reference_the_oracle():
             list((ROOT / "include").glob("*")):
         text = f.read_text()
         assert "liboracle" not in text and "oracle_sort" not in text and "_ref/libref" not in text, f
+
+
+def test_reference_harness_cli_builds_and_links():
+    """tools/rsort_cli: the reference main (Parallel7.cu:696-775) on include/radixsort.hpp."""
+    import subprocess
+    cli = ROOT / "tools" / "rsort_cli"
+    assert cli.exists(), "built by __graft_entry__.build()"
+    out = subprocess.run(["ldd", str(cli)], capture_output=True, text=True).stdout
+    assert "librsort.so" in out and "not found" not in out.split("librsort.so")[1].split("\n")[0]
+
+
+def test_compat_header_compiles_with_reference_style_main(tmp_path):
+    """A Parallel*.cu-style caller (own sortByHost + main, the reference's sort() signature and
+    default arguments) compiles and links unchanged against radixsort.hpp + librsort.so."""
+    import subprocess
+    src = tmp_path / "caller.cpp"
+    src.write_text(r'''
+#include "radixsort.hpp"
+#include <string.h>
+void sortByHost(const uint32_t *in, int n, uint32_t *out, int nBits) { memcpy(out, in, n * 4); (void)nBits; }
+int main() {
+    uint32_t in[4] = {3, 1, 2, 0}, out[4];
+    sort(in, 4, out);                       // default SORT_BY_HOST, numBits = 4, blockSize = 1
+    sort(in, 4, out, SORT_BY_DEVICE, 8, 512);
+    sort(in, 4, out, SORT_BY_THRUST);
+    return 0;
+}
+''')
+    exe = tmp_path / "caller"
+    cmd = ["g++", "-std=c++17", f"-I{ROOT / 'include'}", str(src), "-o", str(exe),
+           f"-L{PKG}", "-lrsort", f"-Wl,-rpath,{PKG}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

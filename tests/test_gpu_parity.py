@@ -278,3 +278,19 @@ def test_partition_stable(nb):
     assert np.array_equal(host(vo), v[order])
     exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
     assert np.array_equal(host(starts), exp)
+
+
+# ------------------------------------------------------------------ reference harness (CLI)
+@pytest.mark.parametrize("args", [["--debug"], [], ["512", "4"], ["256", "5", "--n", "1000003"]])
+def test_reference_harness_cli(args):
+    """tools/rsort_cli reproduces the reference main's flow and prints (Parallel7.cu:696-775):
+    host, Thrust(rocPRIM) and device sorts of glibc rand() keys, each CORRECT."""
+    import subprocess
+    from pathlib import Path
+    cli = Path(__file__).resolve().parent.parent / "tools" / "rsort_cli"
+    r = subprocess.run([str(cli), *args, "--strict"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    out = r.stdout
+    assert out.count("CORRECT :)") == 2 and "INCORRECT" not in out
+    for line in ("Radix Sort by host", "Radix Sort by Thrust library", "Radix Sort by device:", "Time: "):
+        assert line in out
