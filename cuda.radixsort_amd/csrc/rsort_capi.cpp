@@ -90,13 +90,15 @@ int device_cus() {
     return c;
 }
 
-// Tile geometry for one sort: long digit runs (16384-key tiles) for k = 5..8, 8192-key tiles
-// for k <= 4 keys, 4096-key tiles otherwise -- and 4096-key tiles whenever the input is too
-// small to give every CU two large tiles.
+// Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
+// 8192-key tiles (rs_scatter_lines) and pairs use 16384-key tiles (long digit runs); k <= 4 keys
+// use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
+// CU two large tiles.
 int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
-    if (k >= 5 && k <= 8 && n >= enough * geom_tile_keys(kGeomLarge)) return kGeomLarge;
+    if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
+    if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLarge)) return kGeomLarge;
     if (k <= 4 && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     return kGeomSmall;
 }
@@ -121,7 +123,7 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
     if (tpc == 0) {
         // one resident wave of workgroups: as many chunks as the scatter kernel keeps resident
-        int bpc = cus > 0 ? scatter_blocks_per_cu(k, pairs, partition ? RSORT_RANK_MATCH : rank, geom) : 0;
+        int bpc = cus > 0 ? scatter_blocks_per_cu(k, pairs, internal_rank(partition ? RSORT_RANK_MATCH : rank), geom) : 0;
         if (bpc <= 0) bpc = 2;
         const int64_t target = std::max<int64_t>(1, (int64_t)(cus > 0 ? cus : 256) * bpc);
         tpc = (tiles + target - 1) / target;
@@ -204,18 +206,19 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     a.local_only = local_only ? 1u : 0u;
     a.nsplit = (uint32_t)nsplit;
     for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
-    const int rank = (dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH;
-    const int geom = geom_from_shape(p.threads, p.tile_keys);
+    const int rank = internal_rank((dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH);
+    const int geom = geom_from_shape(p.threads, p.tile_keys, p.k_bits, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
+    const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
-    return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, a, s));
+    return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, local_only ? 0 : aligned16, a, s));
 }
 
 int check_plan(const rsort_plan *p) {
     if (!p) return RSORT_ERR_ARG;
     if (p->k_bits < kMinBits || p->k_bits > kMaxBits) return RSORT_ERR_BITS;
     if (p->n < 0 || p->n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
-    if (geom_from_shape(p->threads, p->tile_keys) < 0) return RSORT_ERR_ARG;
+    if (geom_from_shape(p->threads, p->tile_keys, p->k_bits, p->pairs) < 0) return RSORT_ERR_ARG;
     if (p->tiles_per_chunk <= 0 || p->num_chunks <= 0 ||
         p->num_chunks * p->tiles_per_chunk * p->tile_keys < p->n ||
         p->chunk_keys != p->tiles_per_chunk * p->tile_keys || p->bins != (1 << p->k_bits) ||
@@ -461,12 +464,18 @@ int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_keys_in, con
 }
 
 int rsort_set_rank_algo(int algo) {
-    if (algo != RSORT_RANK_MATCH && algo != RSORT_RANK_SPLIT) return RSORT_ERR_ARG;
+    if (algo != RSORT_RANK_MATCH && algo != RSORT_RANK_SPLIT && algo != RSORT_RANK_BALLOT) return RSORT_ERR_ARG;
     g_rank_algo.store(algo);
     return RSORT_OK;
 }
 
 int rsort_get_rank_algo(void) { return g_rank_algo.load(); }
+
+int rsort_lane_order_probe(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return -RSORT_ERR_NODEV;
+    return lane_order_probe();
+}
 
 int rsort_profile_begin(void) {
     std::lock_guard<std::mutex> g(g_prof.mu);

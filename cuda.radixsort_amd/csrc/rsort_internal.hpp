@@ -21,18 +21,31 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // (dev/scatter_lab): the digit runs a tile writes must be long enough to fill 128-B lines, so
 // k = 5..8 uses 16384-key tiles; k <= 4 has long runs already; k >= 9 and small inputs use
 // 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
-enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomCount = 3 };
+// kGeomLines (k = 5..8 keys): 8192-key tiles written as whole 64-B lines (rs_scatter_lines).
+enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomCount = 4 };
 struct GeomShape {
     int threads;
     int kpt;
 };
-constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {512, 16}};
+constexpr int kLineKeys = 16;  // rs_scatter_lines line: 16 keys = 64 B
 inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
-inline int geom_from_shape(int threads, int tile_keys) {
+// K4 and Lines share a shape; the digit width tells them apart.
+inline int geom_from_shape(int threads, int tile_keys, int k_bits, int pairs) {
     for (int g = 0; g < kGeomCount; ++g)
-        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) return g;
+        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) {
+            if (g == kGeomK4 && k_bits >= 5 && k_bits <= 8 && !pairs) return kGeomLines;
+            return g;
+        }
     return -1;
 }
+
+// Internal ranking variants (rs_scatter's RANK template argument).
+enum RankAlgo : int { kRankMatch = 0, kRankSplit = 1, kRankMatchRW = 2, kRankCount = 3, kRankAtomic = 4 };
+// Public rsort_rank_algo -> internal variant for the current device (probes lane order once).
+int internal_rank(int public_algo);
+// 1 / 0: same-address ds_add_rtn lanes are served in lane order on the current device; < 0 error.
+int lane_order_probe();
 
 struct HistArgs {
     const uint32_t *keys;
@@ -71,7 +84,9 @@ struct ScanArgs {
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.
 hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t s);
-hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom,
+// rank_algo: internal RankAlgo. aligned16: kout/vout 16-B aligned (kGeomLines line stores;
+// otherwise the same plan runs rs_scatter with the same tiles).
+hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom, int aligned16,
                           const ScatterArgs &a, hipStream_t s);
 // Whether a (bits, pairs, rank_algo, dmode, geom) scatter kernel is compiled in.
 bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom);

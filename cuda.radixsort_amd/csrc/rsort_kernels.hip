@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "rsort_internal.hpp"
 
 // Diagnostic phase stamps (dev/scatter_lab only; compiled out of the library): wave 0 of each
@@ -56,7 +58,6 @@
 
 namespace rsort {
 
-enum RankAlgo : int { kRankMatch = 0, kRankSplit = 1, kRankMatchRW = 2, kRankCount = 3 };
 
 // ------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -250,10 +251,12 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 //   MINW  minimum waves per SIMD requested from the register allocator (0 = compiler's choice)
 //   ABL   ablation bits for dev/scatter_lab only (1 = skip ranking, 2 = skip global stores)
 template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW = 0,
-          bool DEST = false, int ABL = 0, bool WC = false>
+          bool DEST = false, int ABL = 0, int WCG = 0>
 __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(ScatterArgs a) {
+    constexpr bool WC = WCG > 0;
     static_assert(!(DEST && PAIRS), "DEST staging is for keys-only sorts");
-    static_assert(!WC || (RANK == kRankCount && (1u << BITS) <= (uint32_t)THREADS),
+    constexpr bool COUNT_FIRST = (RANK == kRankCount || RANK == kRankAtomic);
+    static_assert(!WC || (COUNT_FIRST && (1u << BITS) <= (uint32_t)THREADS && (WCG == 16 || WCG == 32)),
                   "write-combining needs the count-first ranking and one digit per thread");
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -261,8 +264,8 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     constexpr uint32_t T = THREADS * KPT;       // tile keys
     constexpr int DPT = (R > THREADS) ? (int)(R / THREADS) : 1;  // digits owned per thread
     constexpr bool MATCH = (RANK == kRankMatch || RANK == kRankMatchRW);
-    static_assert(RANK != kRankCount || !DEST, "kRankCount writes keys during ranking");
-    constexpr uint32_t NCNT = (MATCH || RANK == kRankCount) ? W * R : R;
+    static_assert(!COUNT_FIRST || !DEST, "count-first ranking writes keys during ranking");
+    constexpr uint32_t NCNT = (MATCH || COUNT_FIRST) ? W * R : R;
 
     __shared__ uint32_t s_keys[T];
     __shared__ uint32_t s_vals[PAIRS ? T : 1];
@@ -271,14 +274,14 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     __shared__ uint32_t s_cnt[NCNT];
     __shared__ uint32_t s_delta[WC ? 1 : R];
     __shared__ uint32_t s_ws[W];
-    // write-combining state (WC): per-digit carry of <= 31 keys that did not fill a 128-B line,
-    // its count | invalid-prefix << 8, the new-carry copy spec, and the tile's line records
-    // {global line start, tile source start, digit, carry count | invalid-prefix << 8}
-    __shared__ uint32_t s_carry[WC ? R * 32 : 1];
-    __shared__ uint32_t s_cvals[WC && PAIRS ? R * 32 : 1];
-    __shared__ uint32_t s_cc[WC ? R : 1];
-    __shared__ uint32_t s_nc[WC ? R : 1];
-    __shared__ uint4 s_line[WC ? T / 32 + R : 1];
+    // write-combining state (WC): each digit's carry -- the < WCG keys past its last whole
+    // line, held back until the next tile completes that line -- and per tile: {delta, lim}
+    // (run key at LDS i goes to delta + i if i < lim, else to carry slot i - lim) and
+    // {A, f} (carry slots q < f are flushed to A + q this tile)
+    __shared__ uint32_t s_carry[WC ? R * WCG : 1];
+    __shared__ uint32_t s_cvals[WC && PAIRS ? R * WCG : 1];
+    __shared__ uint2 s_info[WC ? R : 1];
+    __shared__ uint2 s_flush[WC ? R : 1];
 
     const uint32_t t = threadIdx.x;
     const uint32_t w = t / kWave;
@@ -327,11 +330,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
-    if constexpr (WC) {
-        // the chunk's first line of each digit starts (run & 31) keys early: those slots belong to
-        // the previous chunk and are marked invalid (never written by this workgroup)
-        if (t < R && !a.local_only) s_cc[t] = (run[0] & 31u) * 0x101u;
-    }
+    uint32_t wc_c = 0;  // WC: carry count of digit t (the chunk's first line is written partial)
 
     RS_STAMP_DECL
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
@@ -347,13 +346,13 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
         RS_STAMP_WAIT_LOADS();
         RS_STAMP(0);  // waiting for this tile's keys (and the previous tile's stores)
 
-        if constexpr (RANK != kRankCount) {
+        if constexpr (!COUNT_FIRST) {
             for (uint32_t i = t; i < NCNT; i += THREADS) s_cnt[i] = 0;
             __syncthreads();
         }
         RS_STAMP(1);  // counter reset + barrier
 
-        if constexpr (RANK == kRankCount) {
+        if constexpr (COUNT_FIRST) {
             // ---- 0. each wave clears its own counters: no other wave touches s_cnt[w][*]
             //      between the previous tile's digit scan (behind two barriers) and this point
 #pragma unroll
@@ -363,10 +362,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             for (int j = 0; j < KPT; ++j) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
             __syncthreads();
             RS_STAMP(2);  // histogram
-            // ---- 2. digit scan: s_cnt[w][d] <- tile position of wave w's first key of digit d.
-            // With WC, each digit's output is cut into whole 128-B lines: its previous-tile carry
-            // (c keys, line-aligned start A = g - c) + this tile's run, minus the new tail carry.
-            // One packed scan yields both the digit starts (low 16 bits) and line offsets (high).
+            // ---- 2. digit scan: s_cnt[w][d] <- tile position of wave w's first key of digit d
             uint32_t tot[DPT];
             uint32_t mine = 0;
 #pragma unroll
@@ -384,27 +380,9 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                 tot[i] = acc;
                 mine += acc;
             }
-            uint32_t wc_A = 0, wc_c = 0, wc_inv = 0, wc_nfull = 0, wc_leff = 0, wc_ccn = 0;
-            if constexpr (WC) {
-                if (t < R) {
-                    const uint32_t d = t;
-                    // padding (last tile only) has the largest digit and sits at its run's end
-                    wc_leff = tot[0];
-                    if (valid < T && d == dig(0xFFFFFFFFu)) wc_leff -= T - valid;
-                    const uint32_t cc = s_cc[d];
-                    wc_c = cc & 0xFFu;
-                    wc_inv = cc >> 8;
-                    const uint32_t g = run[0];
-                    wc_A = g - wc_c;
-                    const uint32_t e = g + wc_leff;
-                    const uint32_t fe = e & ~31u;
-                    wc_nfull = fe > wc_A ? (fe - wc_A) >> 5 : 0u;
-                    mine |= wc_nfull << 16;
-                }
-            }
             uint32_t all;
-            const uint32_t pstart = block_excl_scan<THREADS>(mine, s_ws, all);
-            uint32_t start = WC ? (pstart & 0xFFFFu) : pstart;
+            uint32_t start = block_excl_scan<THREADS>(mine, s_ws, all);
+            const bool last_tile = nb >= cend;
 #pragma unroll
             for (int i = 0; i < DPT; ++i) {
                 const uint32_t d = t * DPT + i;
@@ -412,23 +390,18 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 #pragma unroll
                     for (int v = 0; v < W; ++v) s_cnt[v * R + d] += start;
                     if constexpr (WC) {
-                        const uint32_t lo = pstart >> 16;
-                        for (uint32_t k = 0; k < wc_nfull; ++k)
-                            s_line[lo + k] = make_uint4(wc_A + 32u * k, start - wc_c + 32u * k, d,
-                                                        k == 0 ? (wc_c | (wc_inv << 8)) : 0u);
-                        // the new tail carry: what is left of carry + run after the whole lines
-                        const uint32_t e = run[i] + wc_leff;
-                        uint32_t cnew, inew;
-                        if (wc_nfull > 0) {
-                            cnew = e & 31u;
-                            inew = 0;
-                            s_nc[d] = (start + wc_leff - cnew) | (cnew << 24);
-                        } else {
-                            cnew = wc_c + wc_leff;
-                            inew = wc_inv;
-                            s_nc[d] = start | (wc_c << 16) | (wc_leff << 24);
-                        }
-                        wc_ccn = cnew | (inew << 8);
+                        // pending output of digit d = its carry (c keys from A = g - c) followed
+                        // by this tile's run; write up to the last whole line (all of it on the
+                        // chunk's last tile), carry the rest. When anything is written, the
+                        // whole old carry is (it lies below the first line end past A).
+                        uint32_t leff = tot[i];  // padding (last tile only) ends the largest digit's run
+                        if (valid < T && d == dig(0xFFFFFFFFu)) leff -= T - valid;
+                        const uint32_t g = run[i], c = wc_c, A = g - c, e = g + leff;
+                        const uint32_t fe = e & ~(uint32_t)(WCG - 1);
+                        const uint32_t Wend = last_tile ? e : (fe > A ? fe : A);
+                        s_info[d] = make_uint2(g - start, start + (Wend - g));  // lim may wrap below start
+                        s_flush[d] = make_uint2(A, Wend > A ? c : 0u);
+                        wc_c = e - Wend;
                         run[i] = e;
                     } else {
                         s_delta[d] = run[i] - start;
@@ -439,12 +412,37 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             }
             __syncthreads();
             RS_STAMP(3);  // barrier + digit scan
-            // ---- 3. peer-match each slot; the counter IS the destination: write the key now
+            if constexpr (WC) {
+                // ---- 2b. flush the old carries that complete a line this tile
+                if (!a.local_only) {
+#pragma unroll 4
+                    for (uint32_t item = tl; item < R * WCG; item += THREADS) {
+                        const uint2 fl = s_flush[item / WCG];
+                        const uint32_t q = item % WCG;
+                        if (q < fl.y) {
+                            a.kout[fl.x + q] = s_carry[item];
+                            if constexpr (PAIRS) a.vout[fl.x + q] = s_cvals[item];
+                        }
+                    }
+                }
+            }
+            // ---- 3. rank each slot; the counter IS the destination: write the key now
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 // recompute the digit: CSE with the histogram step would keep KPT addresses alive
                 asm volatile("" : "+v"(key[j]));
                 const uint32_t d = dig(key[j]);
+                if constexpr (RANK == kRankAtomic) {
+                    // one returning LDS add per key: gfx950 serves the lanes of a ds_add_rtn_u32
+                    // that hit the same address in ascending lane order, so lane l receives
+                    // base + (#lower lanes with its digit) -- the stable rank, with no ballots.
+                    // (verified on every digit width / layout: dev/lds_order_lab.hip; the
+                    // library re-checks it per device before selecting this path)
+                    const uint32_t p = atomicAdd(&s_cnt[w * R + d], 1u);
+                    s_keys[p] = key[j];
+                    if constexpr (PAIRS) s_vals[p] = val[j];
+                    continue;
+                }
                 uint32_t mlo, mhi;
                 peer_mask<BITS>(d, mlo, mhi);
                 const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
@@ -466,38 +464,28 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                     }
                 }
             } else if constexpr (WC) {
-                // ---- 4. whole aligned lines only: 32 lanes per 128-B line, 2 lines per wave store
-                const uint32_t nl = all >> 16;
-#pragma unroll 8
-                for (uint32_t item = tl; item < nl * 32u; item += THREADS) {
-                    const uint4 rec = s_line[item >> 5];
-                    const uint32_t q = item & 31u;
-                    const bool from_carry = q < (rec.w & 0xFFu);
-                    const uint32_t k = from_carry ? s_carry[rec.z * 32u + q] : s_keys[rec.y + q];
-                    uint32_t v = 0;
-                    if constexpr (PAIRS) v = from_carry ? s_cvals[rec.z * 32u + q] : s_vals[rec.y + q];
-                    if constexpr ((ABL & 2) != 0) {
-                        asm volatile("" ::"v"(k), "v"(v));
-                        continue;
+                // ---- 4. run keys below lim complete lines: store; the rest become the carry
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = tl + j * THREADS;
+                    if (valid == T || (uint32_t)(j * THREADS) < olim) {
+                        const uint32_t k = s_keys[i];
+                        const uint32_t d = dig(k);
+                        const uint2 info = s_info[d];
+                        if ((int)(i - info.y) < 0) {
+                            if constexpr ((ABL & 2) != 0) {
+                                asm volatile("" ::"v"(k), "v"(info.x));
+                                continue;
+                            }
+                            a.kout[info.x + i] = k;
+                            if constexpr (PAIRS) a.vout[info.x + i] = s_vals[i];
+                        } else {
+                            s_carry[d * WCG + (i - info.y)] = k;
+                            if constexpr (PAIRS) s_cvals[d * WCG + (i - info.y)] = s_vals[i];
+                        }
                     }
-                    if (q >= (rec.w >> 8)) {  // first line of a chunk: slots below belong to the previous chunk
-                        a.kout[rec.x + q] = k;
-                        if constexpr (PAIRS) a.vout[rec.x + q] = v;
-                    }
+                    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
                 }
-                __syncthreads();  // every old carry has been read
-                // ---- 5. save the new tail carries (<= 31 keys per digit)
-#pragma unroll 8
-                for (uint32_t item = tl; item < R * 32u; item += THREADS) {
-                    const uint32_t d = item >> 5, x = item & 31u;
-                    const uint32_t nc = s_nc[d];
-                    if (x < (nc >> 24)) {
-                        const uint32_t dst = d * 32u + ((nc >> 16) & 0xFFu) + x;
-                        s_carry[dst] = s_keys[(nc & 0xFFFFu) + x];
-                        if constexpr (PAIRS) s_cvals[dst] = s_vals[(nc & 0xFFFFu) + x];
-                    }
-                }
-                if (t < R) s_cc[t] = wc_ccn;
             } else {
                 const bool full = valid == T;
 #pragma unroll
@@ -728,29 +716,234 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             if (nb < cend) load_tile(nb, key, val);
         }
     }
-    if constexpr (WC) {
-        if (!a.local_only) {
-            // ---- chunk end: flush every digit's tail carry (a partial line shared with the next chunk)
-            __syncthreads();                    // the last tile's carry copy is complete
-            if (t < R) s_nc[t] = run[0];        // end of this chunk's output for digit t
-            __syncthreads();
-            for (uint32_t item = t; item < R * 32u; item += THREADS) {
-                const uint32_t d = item >> 5, x = item & 31u;
-                const uint32_t cc = s_cc[d];
-                const uint32_t c = cc & 0xFFu;
-                if (x < c && x >= (cc >> 8)) {
-                    const uint32_t gpos = s_nc[d] - c + x;
-                    a.kout[gpos] = s_carry[d * 32u + x];
-                    if constexpr (PAIRS) a.vout[gpos] = s_cvals[d * 32u + x];
+    RS_STAMP_FLUSH();
+}
+
+// ------------------------------------------------------------------------------ small kernels
+// starts[d] = scanned table[d][0] (global start of digit d), starts[bins] = n.
+// ------------------------------------------------------------------------------ scatter (line-combining)
+// rs_scatter_lines: the same pass as rs_scatter (Parallel7.cu:193-316 fused), built so that every
+// global store is a whole, aligned 128-B line written by ONE 16-B-per-lane store instruction.
+// A digit's output region inside a chunk is contiguous, but each tile ends it mid-line; writing
+// those partial lines costs as much HBM time as whole ones (dev/wc_lab.hip: 1.7 ms aligned vs
+// 2.8 ms misaligned for the same 8 GB). So each digit carries the < G keys past its last whole
+// line into the next tile (the chunk's last tile writes everything).
+//
+// Per tile (count-first ranking, one returning LDS atomic per key -- see kRankAtomic):
+//   1. per-wave digit histogram (non-returning LDS adds)
+//   2. per digit: pending output = carry (c keys from the line-aligned A = g - c) + this tile's
+//      run; it occupies an LDS segment [S, S + sz) whose start is line-aligned, so LDS line
+//      L <-> one global line. The old carry is copied into the segment head, each segment line
+//      gets a record {global key index, valid lanes lo..hi}, and the per-wave counters start
+//      after the carry.
+//   3. rank + stage: P = atomicAdd(counter) is the key's LDS slot; slots past the last whole
+//      line (P >= lim) go to the digit's carry instead
+//   4. output: 4 keys per lane, ds_read_b128 + global_store_dwordx4, G/4 lanes per line
+// At a chunk's start the carry is the (invalid) part of the first line that precedes the
+// chunk's output, so that line is written with a lane mask; after the chunk's last tile the
+// remaining carries are flushed with masked dword stores (both lines are shared with the
+// neighbouring chunks' output).
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE>
+__global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int W = THREADS / kWave;
+    constexpr int SEG = kWave * KPT;
+    constexpr uint32_t T = THREADS * KPT;
+    constexpr uint32_t TPD = THREADS / R;            // threads per digit
+    constexpr uint32_t CAP = T + (G - 1) * R;        // staged keys incl. carries, worst case
+    constexpr uint32_t NL = (CAP + G - 1) / G;
+    constexpr uint32_t QPL = G / 4;                  // 16-B quads per line
+    static_assert(R <= THREADS && TPD <= kWave && (G == 16 || G == 32),
+                  "a digit's thread group lies in one wave; 64/128-B lines");
+
+    __shared__ __attribute__((aligned(16))) uint32_t s_keys[CAP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_vals[PAIRS ? CAP : 4];
+    __shared__ uint32_t s_carry[R * G];
+    __shared__ uint32_t s_cvals[PAIRS ? R * G : 1];
+    __shared__ uint32_t s_cnt[W * R];
+    __shared__ uint32_t s_lim[R];
+    __shared__ uint2 s_line[NL];
+    __shared__ uint2 s_flush[R];  // chunk end: {A, inv | carry << 8}
+    __shared__ uint32_t s_ws[W];
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = t / kWave;
+    const uint32_t lane = lane_id();
+    const uint32_t c = blockIdx.x;
+    const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
+    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+
+    // digit group of this thread: digit d = t / TPD, the group leader (sub == 0) keeps its state
+    const uint32_t d_own = t / TPD;
+    const uint32_t sub = t % TPD;
+    const bool leader = sub == 0;
+    const uint32_t glead = lane & ~(TPD - 1u);       // the leader's lane (TPD <= 64)
+    uint32_t g_run = 0, carry = 0, inv = 0;           // leader state
+    if (leader) {
+        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
+        carry = g & (G - 1u);                          // first line starts before the chunk's output
+        inv = carry;
+        g_run = g;
+    }
+
+    const uint32_t base = w * SEG + lane;
+    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const uint32_t *__restrict__ tk = a.kin + tb;
+        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb : nullptr;
+        if (valid == T) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                k[j] = tk[base + j * kWave];
+                if constexpr (PAIRS) v[j] = tv[base + j * kWave];
+            }
+        } else {
+            const uint32_t lim = valid > base ? valid - base : 0u;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool in = (uint32_t)(j * kWave) < lim;
+                k[j] = in ? tk[base + j * kWave] : 0xFFFFFFFFu;
+                if constexpr (PAIRS) v[j] = in ? tv[base + j * kWave] : 0u;
+            }
+        }
+    };
+
+    uint32_t key[KPT];
+    uint32_t val[PAIRS ? KPT : 1];
+    if (cbeg < cend) load_tile(cbeg, key, val);
+
+    RS_STAMP_DECL
+    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const uint64_t nb = tb + T;
+        // slot j of this lane is a real key iff j * 64 < plim (padding is neither counted nor staged)
+        uint32_t plim = valid > base ? valid - base : 0u;
+        asm volatile("" : "+v"(plim));
+        RS_STAMP_WAIT_LOADS();
+        RS_STAMP(0);
+        // ---- 1. per-wave digit histogram (each wave clears its own counters first)
+#pragma unroll
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+            if (valid == T || (uint32_t)(j * kWave) < plim) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+        __syncthreads();
+        RS_STAMP(2);
+
+        // ---- 2. segments, line records, carry copy, counter bases
+        uint32_t cnt = 0, sz = 0, wcnt = 0, A = 0, e = 0;
+        if (leader) {
+            const uint32_t d = d_own;
+#pragma unroll
+            for (int v = 0; v < W; ++v) {
+                const uint32_t x = s_cnt[v * R + d];
+                s_cnt[v * R + d] = cnt;
+                cnt += x;
+            }
+            A = g_run - carry;    // line-aligned
+            e = g_run + cnt;
+            wcnt = max(A, e & ~(uint32_t)(G - 1)) - A;  // whole lines only: a multiple of G
+            sz = wcnt;
+        }
+        uint32_t nseg;
+        const uint32_t S = block_excl_scan<THREADS>(sz, s_ws, nseg);
+        // broadcast the leader's values to its group
+        const uint32_t gS = __shfl(S, glead), gA = __shfl(A, glead), gw = __shfl(wcnt, glead);
+        const uint32_t gc = __shfl(carry, glead), ginv = __shfl(inv, glead);
+        {
+            const uint32_t d = d_own;
+            // old carry -> segment head (only when something is written; else it stays and grows)
+            if (gw > 0) {
+                for (uint32_t x = sub; x < gc; x += TPD) {
+                    s_keys[gS + x] = s_carry[d * G + x];
+                    if constexpr (PAIRS) s_vals[gS + x] = s_cvals[d * G + x];
                 }
+            }
+            // line records
+            const uint32_t nl = (gw + G - 1) / G;
+            for (uint32_t l = sub; l < nl; l += TPD) {
+                const uint32_t lo = l == 0 ? ginv : 0u;
+                s_line[gS / G + l] = make_uint2(gA + l * G, lo | ((uint32_t)G << 8));
+            }
+        }
+        if (leader) {
+            const uint32_t d = d_own;
+#pragma unroll
+            for (int v = 0; v < W; ++v) s_cnt[v * R + d] += S + carry;
+            s_lim[d] = S + wcnt;
+            if (wcnt > 0) inv = 0;
+            carry = carry + (e - g_run) - wcnt;  // pending - written
+            g_run = e;
+            if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
+        }
+        __syncthreads();
+        RS_STAMP(3);
+
+        // ---- 3. rank (lane-ordered returning LDS add) and stage; tails go to the carry
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            asm volatile("" : "+v"(key[j]));
+            if (valid == T || (uint32_t)(j * kWave) < plim) {
+                const uint32_t d = dig(key[j]);
+                const uint32_t p = atomicAdd(&s_cnt[w * R + d], 1u);
+                const uint32_t lim = s_lim[d];
+                if (p < lim) {
+                    s_keys[p] = key[j];
+                    if constexpr (PAIRS) s_vals[p] = val[j];
+                } else {
+                    s_carry[d * G + (p - lim)] = key[j];
+                    if constexpr (PAIRS) s_cvals[d * G + (p - lim)] = val[j];
+                }
+            }
+        }
+        __syncthreads();
+        RS_STAMP(4);
+        if (nb < cend) load_tile(nb, key, val);
+
+        // ---- 4. whole lines out: 4 keys per lane
+        const uint32_t nq = (nseg / G) * QPL;
+#pragma unroll 2
+        for (uint32_t item = t; item < nq; item += THREADS) {
+            const uint32_t L = item / QPL, q = (item % QPL) * 4u;
+            const uint2 rec = s_line[L];
+            const uint32_t lo = rec.y & 0xFFu, hi = rec.y >> 8;
+            const uint4 kv = *reinterpret_cast<const uint4 *>(&s_keys[L * G + q]);
+            uint4 vv;
+            if constexpr (PAIRS) vv = *reinterpret_cast<const uint4 *>(&s_vals[L * G + q]);
+            const uint64_t gp = (uint64_t)rec.x + q;
+            if (lo <= q && q + 4u <= hi) {
+                *reinterpret_cast<uint4 *>(a.kout + gp) = kv;
+                if constexpr (PAIRS) *reinterpret_cast<uint4 *>(a.vout + gp) = vv;
+            } else {
+                const uint32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+#pragma unroll
+                for (uint32_t x = 0; x < 4; ++x)
+                    if (lo <= q + x && q + x < hi) a.kout[gp + x] = ks[x];
+                if constexpr (PAIRS) {
+                    const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+                    for (uint32_t x = 0; x < 4; ++x)
+                        if (lo <= q + x && q + x < hi) a.vout[gp + x] = vs[x];
+                }
+            }
+        }
+        RS_STAMP(5);
+    }
+    // ---- chunk end: the carries (written by the last tile's staging, behind its barrier)
+    if (cbeg < cend) {
+        for (uint32_t item = t; item < R * G; item += THREADS) {
+            const uint2 fl = s_flush[item / G];
+            const uint32_t x = item % G;
+            if ((fl.y & 0xFFu) <= x && x < (fl.y >> 8)) {
+                a.kout[(uint64_t)fl.x + x] = s_carry[item];
+                if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_cvals[item];
             }
         }
     }
     RS_STAMP_FLUSH();
 }
 
-// ------------------------------------------------------------------------------ small kernels
-// starts[d] = scanned table[d][0] (global start of digit d), starts[bins] = n.
 __global__ void rs_gather_starts(const uint32_t *table, uint32_t num_chunks, uint32_t bins,
                                  uint64_t n, uint32_t *starts) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -830,11 +1023,19 @@ static void *scatter_fn() {
     return reinterpret_cast<void *>(&rs_scatter<BITS, TH, KPT, PAIRS, RANK, DMODE, MINW>);
 }
 
+// count-first ranking: rank = kRankAtomic (lane-ordered LDS adds) or kRankCount (ballots)
+template <int BITS, bool PAIRS, int DMODE, int G>
+static void *scatter_cf(int rank) {
+    return rank == kRankAtomic ? scatter_fn<BITS, PAIRS, kRankAtomic, DMODE, G>()
+                               : scatter_fn<BITS, PAIRS, kRankCount, DMODE, G>();
+}
+
 template <int BITS, bool PAIRS>
-static void *scatter_pick2(int rank, int dmode, int geom) {
+static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
+    if (rank != kRankSplit && rank != kRankAtomic && rank != kRankCount) return nullptr;
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
-            if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankCount, kDigitSplit, kGeomSmall>();
+            if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
         }
         return nullptr;
     }
@@ -842,37 +1043,111 @@ static void *scatter_pick2(int rank, int dmode, int geom) {
         if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankSplit, kDigitShift, kGeomSmall>();
         return nullptr;
     }
-    if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomSmall>();
+    if (geom == kGeomSmall) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
     if constexpr (BITS >= 5 && BITS <= 8) {
-        if (geom == kGeomLarge) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomLarge>();
+        if (geom == kGeomLarge) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLarge>(rank);
+        if constexpr (!PAIRS) {
+            if (geom == kGeomLines) {
+                // whole-line stores need lane-ordered atomics and 16-B aligned outputs; else the
+                // same tiles through rs_scatter
+                if (rank == kRankAtomic && aligned16)
+                    return reinterpret_cast<void *>(
+                        &rs_scatter_lines<BITS, kGeomShape[kGeomLines].threads, kGeomShape[kGeomLines].kpt,
+                                          kLineKeys, false, kDigitShift>);
+                return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLines>(rank);
+            }
+        }
     }
     if constexpr (BITS <= 4 && !PAIRS) {
-        if (geom == kGeomK4) return scatter_fn<BITS, PAIRS, kRankCount, kDigitShift, kGeomK4>();
+        if (geom == kGeomK4) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomK4>(rank);
     }
     return nullptr;
 }
 
 template <int BITS>
-static void *scatter_pick(int pairs, int rank, int dmode, int geom) {
-    return pairs ? scatter_pick2<BITS, true>(rank, dmode, geom) : scatter_pick2<BITS, false>(rank, dmode, geom);
+static void *scatter_pick(int pairs, int rank, int dmode, int geom, int aligned16) {
+    return pairs ? scatter_pick2<BITS, true>(rank, dmode, geom, aligned16)
+                 : scatter_pick2<BITS, false>(rank, dmode, geom, aligned16);
 }
 
-static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom) {
+static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, int aligned16) {
     switch (bits) {
-        case 1: return scatter_pick<1>(pairs, rank, dmode, geom);
-        case 2: return scatter_pick<2>(pairs, rank, dmode, geom);
-        case 3: return scatter_pick<3>(pairs, rank, dmode, geom);
-        case 4: return scatter_pick<4>(pairs, rank, dmode, geom);
-        case 5: return scatter_pick<5>(pairs, rank, dmode, geom);
-        case 6: return scatter_pick<6>(pairs, rank, dmode, geom);
-        case 7: return scatter_pick<7>(pairs, rank, dmode, geom);
-        case 8: return scatter_pick<8>(pairs, rank, dmode, geom);
-        case 9: return scatter_pick<9>(pairs, rank, dmode, geom);
-        case 10: return scatter_pick<10>(pairs, rank, dmode, geom);
-        case 11: return scatter_pick<11>(pairs, rank, dmode, geom);
-        case 12: return scatter_pick<12>(pairs, rank, dmode, geom);
+        case 1: return scatter_pick<1>(pairs, rank, dmode, geom, aligned16);
+        case 2: return scatter_pick<2>(pairs, rank, dmode, geom, aligned16);
+        case 3: return scatter_pick<3>(pairs, rank, dmode, geom, aligned16);
+        case 4: return scatter_pick<4>(pairs, rank, dmode, geom, aligned16);
+        case 5: return scatter_pick<5>(pairs, rank, dmode, geom, aligned16);
+        case 6: return scatter_pick<6>(pairs, rank, dmode, geom, aligned16);
+        case 7: return scatter_pick<7>(pairs, rank, dmode, geom, aligned16);
+        case 8: return scatter_pick<8>(pairs, rank, dmode, geom, aligned16);
+        case 9: return scatter_pick<9>(pairs, rank, dmode, geom, aligned16);
+        case 10: return scatter_pick<10>(pairs, rank, dmode, geom, aligned16);
+        case 11: return scatter_pick<11>(pairs, rank, dmode, geom, aligned16);
+        case 12: return scatter_pick<12>(pairs, rank, dmode, geom, aligned16);
         default: return nullptr;
     }
+}
+
+// ------------------------------------------------------------------------------ lane-order probe
+// Every lane of a wave adds to one of a few LDS counters with a returning atomic and checks the
+// value against the lane-ordered expectation (old + #lower lanes with the same counter).
+__global__ __launch_bounds__(256) void rs_lane_order_probe(uint32_t *bad) {
+    __shared__ uint32_t cnt[4 * 256];
+    const uint32_t t = threadIdx.x, w = t / kWave, lane = lane_id();
+    for (uint32_t i = t; i < 4 * 256; i += 256) cnt[i] = 0;
+    __syncthreads();
+    uint32_t nbad = 0;
+    for (uint32_t it = 0; it < 64; ++it) {
+        uint32_t h = (blockIdx.x * 0x9E3779B9u) ^ (it * 0x85EBCA6Bu) ^ (t * 0xC2B2AE35u);
+        h ^= h >> 16;
+        h *= 0x7feb352dU;
+        h ^= h >> 15;
+        const uint32_t range = (it & 3) == 0 ? 1u : (it & 3) == 1 ? 3u : (it & 3) == 2 ? 16u : 256u;
+        const uint32_t d = h % range;
+        const uint32_t idx = w * 256 + d;
+        const uint32_t before = cnt[idx];
+        uint32_t below = 0;
+        for (int l = 0; l < kWave; ++l) {
+            const uint32_t dl = __shfl(d, l);  // every lane takes part (bpermute reads active lanes only)
+            below += ((uint32_t)l < lane && dl == d) ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t got = atomicAdd(&cnt[idx], 1u);
+        nbad += got != before + below;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+int lane_order_probe() {
+    static std::mutex mu;
+    static int state[64] = {0};  // per device: 0 unknown, 1 ordered, 2 not ordered
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    std::lock_guard<std::mutex> g(mu);
+    if (state[dev]) return state[dev] == 1 ? 1 : 0;
+    hipStream_t s = nullptr;
+    uint32_t *bad = nullptr;
+    uint32_t host = 1;
+    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&bad, 4) == hipSuccess && hipMemsetAsync(bad, 0, 4, s) == hipSuccess;
+    if (ok) {
+        rs_lane_order_probe<<<512, 256, 0, s>>>(bad);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(&host, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+    }
+    if (bad) (void)hipFree(bad);
+    if (s) (void)hipStreamDestroy(s);
+    if (!ok) return -1;
+    state[dev] = host == 0 ? 1 : 2;
+    return host == 0 ? 1 : 0;
+}
+
+int internal_rank(int public_algo) {
+    if (public_algo == 1) return kRankSplit;   // RSORT_RANK_SPLIT
+    if (public_algo == 2) return kRankCount;   // RSORT_RANK_BALLOT
+    return lane_order_probe() == 1 ? kRankAtomic : kRankCount;
 }
 
 hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t s) {
@@ -895,13 +1170,13 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
 
 bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom) {
     if (geom < 0 || geom >= kGeomCount) return false;
-    return scatter_kernel(bits, pairs, rank_algo, dmode, geom) != nullptr;
+    return scatter_kernel(bits, pairs, rank_algo, dmode, geom, 1) != nullptr;
 }
 
-hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom,
+hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom, int aligned16,
                           const ScatterArgs &a, hipStream_t s) {
     if (geom < 0 || geom >= kGeomCount) return hipErrorInvalidValue;
-    void *fn = scatter_kernel(bits, pairs, rank_algo, dmode, geom);
+    void *fn = scatter_kernel(bits, pairs, rank_algo, dmode, geom, aligned16);
     if (!fn) return hipErrorInvalidValue;
     ScatterArgs copy = a;
     void *args[] = {&copy};
@@ -910,7 +1185,7 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
 
 int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom) {
     if (geom < 0 || geom >= kGeomCount) return 0;
-    void *fn = scatter_kernel(bits, pairs, rank_algo, kDigitShift, geom);
+    void *fn = scatter_kernel(bits, pairs, rank_algo, kDigitShift, geom, 1);
     if (!fn) return 0;
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kGeomShape[geom].threads, 0) != hipSuccess)

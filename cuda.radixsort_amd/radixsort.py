@@ -38,7 +38,7 @@ RSORT_OK = 0
 STATUS_NAMES = {0: "RSORT_OK", 1: "RSORT_ERR_ARG", 2: "RSORT_ERR_BITS", 3: "RSORT_ERR_SIZE",
                 4: "RSORT_ERR_ALIGN", 5: "RSORT_ERR_ALLOC", 6: "RSORT_ERR_HIP",
                 7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV"}
-RANK_MATCH, RANK_SPLIT = 0, 1
+RANK_MATCH, RANK_SPLIT, RANK_BALLOT = 0, 1, 2
 PHASES = ("histogram", "scan", "scatter", "copy")
 
 
@@ -101,6 +101,7 @@ SIGNATURES = {
     "rsort_pass_local_sort": ([_PP, _vp, _vp, _vp, _vp, _int, _vp], _int),
     "rsort_set_rank_algo": ([_int], _int),
     "rsort_get_rank_algo": ([], _int),
+    "rsort_lane_order_probe": ([], _int),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
     "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
@@ -285,6 +286,15 @@ def set_rank_algo(algo: int):
 
 def get_rank_algo() -> int:
     return int(_lib().rsort_get_rank_algo())
+
+
+def lane_order_probe() -> int:
+    """1 if the current device serves same-address LDS atomic lanes in lane order (the default
+    ranking then uses one returning LDS add per key), 0 if not (ballot ranking)."""
+    r = int(_lib().rsort_lane_order_probe())
+    if r < 0:
+        raise RSortError(-r if r < -1 else 5, "rsort_lane_order_probe")
+    return r
 
 
 @contextmanager

@@ -65,11 +65,26 @@ float time_ms(Ctx &c, int reps, F f) {
 
 static const char *g_filter = nullptr;
 
+template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
+void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift = 0, int reps = 5);
+
 template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int MINW, bool DEST = false, int ABL = 0,
-          bool WC = false>
+          int WCG = 0>
 void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
+    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
+                                          rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, kDigitShift, MINW, DEST, ABL, WCG>,
+                                          shift, reps);
+}
+
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS>
+void lines(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
+    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult, rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift>,
+                                          shift, reps);
+}
+
+template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
+void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, int reps) {
     if (g_filter && !strstr(name, g_filter)) return;
-    auto kern = rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, kDigitShift, MINW, DEST, ABL, WC>;
     int bpc = 0;
     CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, THREADS, 0));
     const uint64_t T = (uint64_t)THREADS * KPT;
@@ -168,11 +183,35 @@ int main(int argc, char **argv) {
     constexpr int M = kRankMatch;
     constexpr int RW = kRankMatchRW;
     constexpr int CT = kRankCount;
+    constexpr int AT = kRankAtomic;
     variant<8, 256, 16, false, M, 0>(c, "k8 256x16 match (ref)", 1.0);
     variant<8, 256, 16, false, CT, 0>(c, "k8 256x16 count", 1.0);
     variant<8, 256, 32, false, CT, 0>(c, "k8 256x32 count", 1.0);
     variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count", 1.0);
     variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count x2", 2.0);
+    variant<8, 512, 32, false, CT, 0, false, 2>(c, "k8 512x32 count nostore", 1.0);
+    variant<8, 512, 32, false, AT, 0>(c, "k8 512x32 atomic", 1.0);
+    variant<8, 512, 32, false, AT, 0>(c, "k8 512x32 atomic x2", 2.0);
+    variant<8, 512, 32, false, AT, 0, false, 2>(c, "k8 512x32 atomic nostore", 1.0);
+    variant<8, 256, 32, false, AT, 0>(c, "k8 256x32 atomic", 1.0);
+    variant<8, 512, 16, false, AT, 0>(c, "k8 512x16 atomic", 1.0);
+    variant<8, 256, 16, false, AT, 0>(c, "k8 256x16 atomic", 1.0);
+    variant<8, 512, 16, false, AT, 0, false, 0, 32>(c, "k8 512x16 atomic wc32", 1.0);
+    variant<8, 512, 16, false, AT, 0, false, 0, 16>(c, "k8 512x16 atomic wc16", 1.0);
+    variant<8, 512, 24, false, AT, 0, false, 0, 16>(c, "k8 512x24 atomic wc16", 1.0);
+    variant<8, 512, 32, false, AT, 0, false, 0, 16>(c, "k8 512x32 atomic wc16", 1.0);
+    variant<8, 512, 32, false, AT, 0, false, 0, 32>(c, "k8 512x32 atomic wc32", 1.0);
+    variant<8, 1024, 16, false, AT, 0, false, 0, 32>(c, "k8 1024x16 atomic wc32", 1.0);
+    variant<8, 1024, 24, false, AT, 0, false, 0, 32>(c, "k8 1024x24 atomic wc32", 1.0);
+    variant<8, 256, 32, false, AT, 0, false, 0, 32>(c, "k8 256x32 atomic wc32", 1.0);
+    variant<8, 512, 16, false, AT, 0, false, 2, 32>(c, "k8 512x16 atomic wc32 nostore", 1.0);
+    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32", 1.0);
+    lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
+    lines<8, 512, 16, 32, false>(c, "k8 512x16 lines32", 1.0);
+    lines<8, 512, 16, 16, false>(c, "k8 512x16 lines16", 1.0);
+    lines<8, 512, 24, 16, false>(c, "k8 512x24 lines16", 1.0);
+    lines<8, 1024, 8, 32, false>(c, "k8 1024x8 lines32", 1.0);
+    lines<8, 256, 32, 32, false>(c, "k8 256x32 lines32", 1.0);
     variant<8, 256, 64, false, CT, 0>(c, "k8 256x64 count", 1.0);
     variant<8, 1024, 16, false, CT, 0>(c, "k8 1024x16 count", 1.0);
     c.have_ref = false;
@@ -181,10 +220,23 @@ int main(int argc, char **argv) {
     variant<8, 256, 32, true, RW, 0>(c, "k8 pairs 256x32 matchRW", 1.0);
     variant<8, 512, 16, true, CT, 0>(c, "k8 pairs 512x16 count", 1.0);
     variant<8, 512, 32, true, CT, 0>(c, "k8 pairs 512x32 count", 1.0);
+    variant<8, 512, 32, true, AT, 0>(c, "k8 pairs 512x32 atomic", 1.0);
+    variant<8, 512, 16, true, AT, 0>(c, "k8 pairs 512x16 atomic", 1.0);
+    variant<8, 512, 16, true, AT, 0, false, 0, 32>(c, "k8 pairs 512x16 atomic wc32", 1.0);
+    lines<8, 1024, 8, 16, true>(c, "k8 pairs 1024x8 lines16", 1.0);
+    lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
     c.have_ref = false;
     variant<4, 256, 16, false, M, 0>(c, "k4 256x16 match (ref)", 1.0);
     variant<4, 256, 16, false, CT, 0>(c, "k4 256x16 count", 1.0);
     variant<4, 512, 16, false, CT, 4>(c, "k4 512x16 count w4", 1.0);
     variant<4, 512, 32, false, CT, 0>(c, "k4 512x32 count", 1.0);
+    variant<4, 512, 16, false, AT, 0>(c, "k4 512x16 atomic", 1.0);
+    variant<4, 512, 32, false, AT, 0>(c, "k4 512x32 atomic", 1.0);
+    variant<4, 512, 16, false, AT, 0, false, 0, 32>(c, "k4 512x16 atomic wc32", 1.0);
+    variant<4, 512, 32, false, AT, 0, false, 0, 32>(c, "k4 512x32 atomic wc32", 1.0);
+    lines<4, 1024, 16, 32, false>(c, "k4 1024x16 lines32", 1.0);
+    lines<4, 1024, 32, 32, false>(c, "k4 1024x32 lines32", 1.0);
+    lines<4, 512, 32, 32, false>(c, "k4 512x32 lines32", 1.0);
+    lines<4, 512, 16, 32, false>(c, "k4 512x16 lines32", 1.0);
     return 0;
 }

@@ -61,11 +61,15 @@ typedef enum rsort_status {
     RSORT_ERR_NODEV = 8       /* no HIP device visible */
 } rsort_status;
 
-/* Local-rank algorithm inside a tile (both give the same, unique, stable result). */
+/* Local-rank algorithm inside a tile (all give the same, unique, stable result). */
 typedef enum rsort_rank_algo {
-    RSORT_RANK_MATCH = 0, /* wave64 ballot peer-match + per-wave LDS digit counters (default) */
-    RSORT_RANK_SPLIT = 1  /* k successive block-local 1-bit splits, ballot/popcount scans
-                             (the reference's algorithm, Parallel5.cu:79-159 / P7:79-191) */
+    RSORT_RANK_MATCH = 0,  /* default: per-wave LDS digit counters; a key's rank is one
+                              returning LDS add where the device serves same-address lanes in
+                              lane order (probed once per device, rsort_lane_order_probe),
+                              else the ballot peer-match below */
+    RSORT_RANK_SPLIT = 1,  /* k successive block-local 1-bit splits, ballot/popcount scans
+                              (the reference's algorithm, Parallel5.cu:79-159 / P7:79-191) */
+    RSORT_RANK_BALLOT = 2  /* per-wave LDS digit counters + wave64 ballot peer-match */
 } rsort_rank_algo;
 
 /* Phases reported by the profiler (the reference's MEASURE_PORTION_EXECUTION_TIME buckets,
@@ -160,6 +164,10 @@ RSORT_API int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_ke
 /* ---------------------------------------------------------------- options / profiling */
 RSORT_API int rsort_set_rank_algo(int algo); /* rsort_rank_algo, process-wide */
 RSORT_API int rsort_get_rank_algo(void);
+/* 1 if the current device's LDS returns same-address atomic adds in lane order (the default
+ * ranking relies on it and falls back to ballots otherwise), 0 if not, < 0 on error. The
+ * probe runs once per device (a few microseconds) and is cached. */
+RSORT_API int rsort_lane_order_probe(void);
 /* Between begin and end, every launch made by this library records hipEvents around its
  * phases; end synchronises those events and returns the per-phase sums. */
 RSORT_API int rsort_profile_begin(void);

@@ -48,7 +48,8 @@ def test_plan_geometry(n, k):
     assert p.bins == 1 << k
     assert (p.threads, p.tile_keys) in {(256, 4096), (512, 16384), (512, 8192)}
     if n >= 2 * 256 * 16384 and 5 <= k <= 8:
-        assert p.tile_keys == 16384  # long digit runs for the headline configuration
+        assert p.tile_keys == 8192   # whole-line (rs_scatter_lines) tiles for the headline configuration
+        assert rs.plan(n, k, True).tile_keys == 16384  # pairs: long digit runs
     assert p.chunk_keys == p.tiles_per_chunk * p.tile_keys
     assert p.num_chunks * p.chunk_keys >= n
     assert (p.num_chunks - 1) * p.chunk_keys < max(n, 1)
@@ -56,7 +57,7 @@ def test_plan_geometry(n, k):
     assert p.workspace_bytes >= 4 * n + 4 * p.table_entries
     assert rs.workspace_size(n, k) == p.workspace_bytes
     pp = rs.plan(n, k, True)
-    assert pp.workspace_bytes >= p.workspace_bytes + 4 * n
+    assert pp.workspace_bytes >= 8 * n + 4 * pp.table_entries
 
 
 def test_plan_explicit_tiles_per_chunk():
@@ -87,6 +88,7 @@ def test_device_entry_validates_before_touching_the_gpu():
     # workspace too small
     assert lib.rsort_u32_device(ctypes.c_void_p(256), ctypes.c_void_p(512), 10, 8, ctypes.c_void_p(1024), 16, None) == 7
     assert lib.rsort_set_rank_algo(7) == 1
+    assert lib.rsort_set_rank_algo(3) == 1
     assert lib.rsort_partition_device(None, None, None, None, 10, None, 0, None, None, 0, None) == 1
     assert lib.rsort_partition_device(None, None, None, None, 10, None, 17, None, None, 0, None) == 1
 

@@ -10,7 +10,7 @@ from _util import (fnv1a64, glibc_rand, oracle_block_pass, oracle_sort, oracle_s
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-RANKS = [rs.RANK_MATCH, rs.RANK_SPLIT]
+RANKS = [rs.RANK_MATCH, rs.RANK_SPLIT, rs.RANK_BALLOT]
 
 
 def dev(a):
@@ -113,6 +113,44 @@ def test_large_tile_geometries(k):
         torch.cuda.synchronize()
         rk, rv = oracle_sort_pairs(keys, vals, k)
         assert np.array_equal(host(ko), rk) and np.array_equal(host(vo), rv)
+
+
+def test_lane_order_probe():
+    """The default ranking's hardware premise holds on the MI355X (dev/lds_order_lab.hip)."""
+    assert rs.lane_order_probe() == 1
+
+
+@pytest.mark.parametrize("dist", ["uniform", "zipf", "allsame", "fewdigits"])
+@pytest.mark.parametrize("tpc", [0, 1, 3, 7])
+def test_whole_line_scatter(dist, tpc):
+    """k = 5..8 keys at n >= 2 * CUs * 8192 run rs_scatter_lines (whole 64-B lines, per-digit
+    carries across tiles, masked first/last lines per chunk): chunk geometries, skew, ragged n."""
+    n = (1 << 22) + 4099
+    if dist == "uniform":
+        x = uniform_keys(n, seed=tpc)
+    elif dist == "zipf":
+        x = zipf_keys(n, seed=tpc)
+    elif dist == "allsame":
+        x = np.full(n, 0x12345678, np.uint32)
+    else:
+        x = uniform_keys(n, seed=tpc) & np.uint32(0x03030303)
+    for k in (8, 5, 7):
+        p = rs.plan(n, k, False, tpc)
+        assert p.tile_keys == 8192 and p.threads == 512
+        assert np.array_equal(gpu_sort(x, k, tiles_per_chunk=tpc), oracle_sort(x, k)), (dist, tpc, k)
+
+
+def test_whole_line_scatter_misaligned_output_falls_back():
+    """An output pointer that is 4-B but not 16-B aligned takes the same tiles through
+    rs_scatter (no 16-B line stores); the result is the same."""
+    n = (1 << 22) + 77
+    x = zipf_keys(n, seed=5)
+    big = rs.empty_u32(n + 4)
+    for off in (1, 2, 3):
+        out = big[off:off + n]
+        rs.sort_device(dev(x), out, 8)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(out), oracle_sort(x, 8)), off
 
 
 @pytest.mark.parametrize("tpc", [1, 2, 3, 17])
