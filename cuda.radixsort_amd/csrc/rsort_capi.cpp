@@ -91,7 +91,7 @@ int device_cus() {
 }
 
 // Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
-// 8192-key tiles (rs_scatter_lines) and pairs use 16384-key tiles (long digit runs); k <= 4 keys
+// 16384-key tiles (rs_scatter_lines) and pairs use 16384-key tiles (long digit runs); k <= 4 keys
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
 // CU two large tiles.
 int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
@@ -176,7 +176,15 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     a.vec = (((uintptr_t)keys & 15u) == 0) ? 1u : 0u;
     a.nsplit = (uint32_t)nsplit;
     for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
+    // few, long chunks (one scatter workgroup per CU): several histogram workgroups per chunk,
+    // their counts added into a zeroed table
+    const int cus = device_cus();
+    const int64_t want = 8 * (int64_t)(cus > 0 ? cus : 256);
+    a.split = 1;
+    if (p.num_chunks < want && p.chunk_keys >= 8 * 4096)
+        a.split = (uint32_t)std::min<int64_t>({(want + p.num_chunks - 1) / p.num_chunks, p.chunk_keys / 4096, 64});
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
+    if (a.split > 1 && hipMemsetAsync(table, 0, (size_t)p.table_entries * 4, s) != hipSuccess) return RSORT_ERR_HIP;
     return hip_status(launch_histogram(p.k_bits, dmode, a, s));
 }
 
@@ -207,7 +215,7 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     a.nsplit = (uint32_t)nsplit;
     for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
     const int rank = internal_rank((dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH);
-    const int geom = geom_from_shape(p.threads, p.tile_keys, p.k_bits, p.pairs);
+    const int geom = geom_from_shape(p.threads, p.tile_keys);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
@@ -218,7 +226,7 @@ int check_plan(const rsort_plan *p) {
     if (!p) return RSORT_ERR_ARG;
     if (p->k_bits < kMinBits || p->k_bits > kMaxBits) return RSORT_ERR_BITS;
     if (p->n < 0 || p->n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
-    if (geom_from_shape(p->threads, p->tile_keys, p->k_bits, p->pairs) < 0) return RSORT_ERR_ARG;
+    if (geom_from_shape(p->threads, p->tile_keys) < 0) return RSORT_ERR_ARG;
     if (p->tiles_per_chunk <= 0 || p->num_chunks <= 0 ||
         p->num_chunks * p->tiles_per_chunk * p->tile_keys < p->n ||
         p->chunk_keys != p->tiles_per_chunk * p->tile_keys || p->bins != (1 << p->k_bits) ||

@@ -21,22 +21,19 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // (dev/scatter_lab): the digit runs a tile writes must be long enough to fill 128-B lines, so
 // k = 5..8 uses 16384-key tiles; k <= 4 has long runs already; k >= 9 and small inputs use
 // 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
-// kGeomLines (k = 5..8 keys): 8192-key tiles written as whole 64-B lines (rs_scatter_lines).
+// kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 64-B lines
+// (rs_scatter_lines; one workgroup per CU, its LDS holds the tile plus every digit's carry).
 enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomCount = 4 };
 struct GeomShape {
     int threads;
     int kpt;
 };
-constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {512, 16}};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}};
 constexpr int kLineKeys = 16;  // rs_scatter_lines line: 16 keys = 64 B
 inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
-// K4 and Lines share a shape; the digit width tells them apart.
-inline int geom_from_shape(int threads, int tile_keys, int k_bits, int pairs) {
+inline int geom_from_shape(int threads, int tile_keys) {
     for (int g = 0; g < kGeomCount; ++g)
-        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) {
-            if (g == kGeomK4 && k_bits >= 5 && k_bits <= 8 && !pairs) return kGeomLines;
-            return g;
-        }
+        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) return g;
     return -1;
 }
 
@@ -55,6 +52,7 @@ struct HistArgs {
     uint32_t num_chunks;
     uint32_t shift;
     uint32_t vec;           // keys 16-byte aligned: uint4 loads
+    uint32_t split;         // workgroups per chunk (> 1: partial counts added into a zeroed table)
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
 };

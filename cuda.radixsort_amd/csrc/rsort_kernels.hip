@@ -113,6 +113,25 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_ws, 
     return pre + inc - v;
 }
 
+// Same, with one barrier: the caller guarantees another barrier before s_ws is written again.
+template <int THREADS>
+__device__ __forceinline__ uint32_t block_excl_scan1(uint32_t v, uint32_t *s_ws, uint32_t &total) {
+    constexpr int W = THREADS / kWave;
+    const uint32_t w = threadIdx.x / kWave;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane_id() == kWave - 1) s_ws[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+        const uint32_t s = s_ws[i];
+        pre += ((uint32_t)i < w) ? s : 0u;
+        tot += s;
+    }
+    total = tot;
+    return pre + inc - v;
+}
+
 template <int BITS, int DMODE>
 struct Digit {
     uint32_t shift;
@@ -140,14 +159,20 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     __shared__ uint32_t s_h[HW * R];
 
     const uint32_t t = threadIdx.x;
-    const uint32_t c = blockIdx.x;
+    const uint32_t S = a.split;
+    const uint32_t c = blockIdx.x / S;
+    const uint32_t sub = blockIdx.x % S;
     for (uint32_t i = t; i < HW * R; i += THREADS) s_h[i] = 0;
     __syncthreads();
 
     uint32_t *my = s_h + (HW > 1 ? (t / kWave) * R : 0);
     const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
-    const uint64_t beg = (uint64_t)c * a.chunk_keys;
-    const uint64_t end = min(beg + a.chunk_keys, a.n);
+    // this workgroup's part of chunk c: S parts of a multiple of 4 keys (16-B aligned starts)
+    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
+    const uint64_t beg = min(cbeg + sub * part, cend);
+    const uint64_t end = min(beg + part, cend);
     uint64_t tail = beg;
     if (a.vec) {
         const uint4 *p = reinterpret_cast<const uint4 *>(a.keys + beg);
@@ -178,7 +203,8 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
         uint32_t s = 0;
 #pragma unroll
         for (int w = 0; w < HW; ++w) s += s_h[w * R + d];
-        a.table[(uint64_t)d * a.num_chunks + c] = s;
+        if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = s;
+        else if (s) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], s);
     }
 }
 
@@ -723,26 +749,27 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // starts[d] = scanned table[d][0] (global start of digit d), starts[bins] = n.
 // ------------------------------------------------------------------------------ scatter (line-combining)
 // rs_scatter_lines: the same pass as rs_scatter (Parallel7.cu:193-316 fused), built so that every
-// global store is a whole, aligned 128-B line written by ONE 16-B-per-lane store instruction.
+// global store is a whole, aligned G-key line written by 16-B-per-lane store instructions.
 // A digit's output region inside a chunk is contiguous, but each tile ends it mid-line; writing
 // those partial lines costs as much HBM time as whole ones (dev/wc_lab.hip: 1.7 ms aligned vs
 // 2.8 ms misaligned for the same 8 GB). So each digit carries the < G keys past its last whole
-// line into the next tile (the chunk's last tile writes everything).
+// line into the next tile.
 //
 // Per tile (count-first ranking, one returning LDS atomic per key -- see kRankAtomic):
 //   1. per-wave digit histogram (non-returning LDS adds)
 //   2. per digit: pending output = carry (c keys from the line-aligned A = g - c) + this tile's
-//      run; it occupies an LDS segment [S, S + sz) whose start is line-aligned, so LDS line
-//      L <-> one global line. The old carry is copied into the segment head, each segment line
-//      gets a record {global key index, valid lanes lo..hi}, and the per-wave counters start
-//      after the carry.
+//      run; its whole lines occupy an LDS segment [S, S + wcnt) whose start is line-aligned, so
+//      LDS line L <-> one global line. The old carry is copied into the segment head, each line
+//      gets a record {global key index, first valid lane}, the per-wave counters start after
+//      the carry
 //   3. rank + stage: P = atomicAdd(counter) is the key's LDS slot; slots past the last whole
-//      line (P >= lim) go to the digit's carry instead
+//      line (P >= lim) go to the digit's carry (one store, the address selected)
 //   4. output: 4 keys per lane, ds_read_b128 + global_store_dwordx4, G/4 lanes per line
 // At a chunk's start the carry is the (invalid) part of the first line that precedes the
 // chunk's output, so that line is written with a lane mask; after the chunk's last tile the
 // remaining carries are flushed with masked dword stores (both lines are shared with the
-// neighbouring chunks' output).
+// neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
+// tiles), so the full-tile paths carry no per-slot predicates.
 template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
@@ -751,19 +778,18 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t T = THREADS * KPT;
     constexpr uint32_t TPD = THREADS / R;            // threads per digit
     constexpr uint32_t CAP = T + (G - 1) * R;        // staged keys incl. carries, worst case
-    constexpr uint32_t NL = (CAP + G - 1) / G;
+    constexpr uint32_t NL = CAP / G;
     constexpr uint32_t QPL = G / 4;                  // 16-B quads per line
     static_assert(R <= THREADS && TPD <= kWave && (G == 16 || G == 32),
                   "a digit's thread group lies in one wave; 64/128-B lines");
 
-    __shared__ __attribute__((aligned(16))) uint32_t s_keys[CAP];
-    __shared__ __attribute__((aligned(16))) uint32_t s_vals[PAIRS ? CAP : 4];
-    __shared__ uint32_t s_carry[R * G];
-    __shared__ uint32_t s_cvals[PAIRS ? R * G : 1];
-    __shared__ uint32_t s_cnt[W * R];
+    // staging: [0, CAP) whole lines of every digit, [CAP, CAP + R*G) the per-digit carries
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];  // + padding sink
+    __shared__ __attribute__((aligned(16))) uint32_t s_vstage[PAIRS ? CAP + R * G + 4 : 4];
+    __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
     __shared__ uint32_t s_lim[R];
-    __shared__ uint2 s_line[NL];
-    __shared__ uint2 s_flush[R];  // chunk end: {A, inv | carry << 8}
+    __shared__ uint32_t s_line[NL];   // global key index of the line | first valid lane (< G)
+    __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
 
     const uint32_t t = threadIdx.x;
@@ -774,15 +800,15 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
 
-    // digit group of this thread: digit d = t / TPD, the group leader (sub == 0) keeps its state
+    // digit group of this thread: digit d = t / TPD; the leader (sub == 0) keeps the state
     const uint32_t d_own = t / TPD;
     const uint32_t sub = t % TPD;
     const bool leader = sub == 0;
-    const uint32_t glead = lane & ~(TPD - 1u);       // the leader's lane (TPD <= 64)
-    uint32_t g_run = 0, carry = 0, inv = 0;           // leader state
+    const uint32_t glead = lane & ~(TPD - 1u);
+    uint32_t g_run = 0, carry = 0, inv = 0;
     if (leader) {
         const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
-        carry = g & (G - 1u);                          // first line starts before the chunk's output
+        carry = g & (G - 1u);  // the first line starts before the chunk's output
         inv = carry;
         g_run = g;
     }
@@ -790,21 +816,23 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     const uint32_t base = w * SEG + lane;
     auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        const uint32_t *__restrict__ tk = a.kin + tb;
-        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb : nullptr;
+        uint32_t lb = base;  // opaque: one lane offset + immediate slot offsets, nothing hoisted
+        asm volatile("" : "+v"(lb));
+        const uint32_t *__restrict__ tk = a.kin + tb + lb;
+        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb + lb : nullptr;
         if (valid == T) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                k[j] = tk[base + j * kWave];
-                if constexpr (PAIRS) v[j] = tv[base + j * kWave];
+                k[j] = tk[j * kWave];
+                if constexpr (PAIRS) v[j] = tv[j * kWave];
             }
         } else {
-            const uint32_t lim = valid > base ? valid - base : 0u;
+            const uint32_t lim = valid > lb ? valid - lb : 0u;
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const bool in = (uint32_t)(j * kWave) < lim;
-                k[j] = in ? tk[base + j * kWave] : 0xFFFFFFFFu;
-                if constexpr (PAIRS) v[j] = in ? tv[base + j * kWave] : 0u;
+                k[j] = in ? tk[j * kWave] : 0u;
+                if constexpr (PAIRS) v[j] = in ? tv[j * kWave] : 0u;
             }
         }
     };
@@ -816,119 +844,155 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     RS_STAMP_DECL
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const bool full = valid == T;
         const uint64_t nb = tb + T;
-        // slot j of this lane is a real key iff j * 64 < plim (padding is neither counted nor staged)
-        uint32_t plim = valid > base ? valid - base : 0u;
+        uint32_t plim = valid > base ? valid - base : 0u;  // slot j is real iff j * 64 < plim
         asm volatile("" : "+v"(plim));
         RS_STAMP_WAIT_LOADS();
         RS_STAMP(0);
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
         for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            if (valid == T || (uint32_t)(j * kWave) < plim) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+            for (int j = 0; j < KPT; ++j) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if ((uint32_t)(j * kWave) < plim) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+        }
+        // next tile's keys: in flight through the scan, staging and output phases
+        uint32_t nkey[KPT];
+        uint32_t nval[PAIRS ? KPT : 1];
+        if (nb < cend) load_tile(nb, nkey, nval);
         __syncthreads();
         RS_STAMP(2);
 
         // ---- 2. segments, line records, carry copy, counter bases
-        uint32_t cnt = 0, sz = 0, wcnt = 0, A = 0, e = 0;
-        if (leader) {
-            const uint32_t d = d_own;
+        // the group's TPD threads split the W per-wave counters of digit d; the leader combines
+        constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;   // waves per group thread
+        uint32_t part = 0;
+        uint32_t wx[WPT];
+        if (sub < (uint32_t)W) {
 #pragma unroll
-            for (int v = 0; v < W; ++v) {
-                const uint32_t x = s_cnt[v * R + d];
-                s_cnt[v * R + d] = cnt;
-                cnt += x;
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * R + d_own] : 0u;
+                part += wx[i];
             }
-            A = g_run - carry;    // line-aligned
+        }
+        // exclusive prefix of the parts inside the group and the digit's tile count (the group is
+        // TPD consecutive lanes of one wave)
+        uint32_t gpre = 0, cnt = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < TPD; ++q) {
+            const uint32_t y = __shfl(part, glead + q);
+            if (q < sub) gpre += y;
+            cnt += y;
+        }
+        uint32_t wcnt = 0, A = 0, e = 0;
+        if (leader) {
+            A = g_run - carry;  // line-aligned
             e = g_run + cnt;
-            wcnt = max(A, e & ~(uint32_t)(G - 1)) - A;  // whole lines only: a multiple of G
-            sz = wcnt;
+            wcnt = max(A, e & ~(uint32_t)(G - 1)) - A;  // whole lines only
         }
         uint32_t nseg;
-        const uint32_t S = block_excl_scan<THREADS>(sz, s_ws, nseg);
-        // broadcast the leader's values to its group
-        const uint32_t gS = __shfl(S, glead), gA = __shfl(A, glead), gw = __shfl(wcnt, glead);
-        const uint32_t gc = __shfl(carry, glead), ginv = __shfl(inv, glead);
+        const uint32_t S = block_excl_scan1<THREADS>(wcnt, s_ws, nseg);  // next s_ws write is a tile later
+        const uint32_t gS = __shfl(S, glead), gw = __shfl(wcnt, glead);
+        const uint32_t gA = __shfl(A, glead), gc = __shfl(carry, glead), ginv = __shfl(inv, glead);
         {
             const uint32_t d = d_own;
-            // old carry -> segment head (only when something is written; else it stays and grows)
+            // per-wave counter bases: after the carry, waves in order
+            if (sub < (uint32_t)W) {
+                uint32_t acc = gS + gc + gpre;
+#pragma unroll
+                for (uint32_t i = 0; i < WPT; ++i) {
+                    const uint32_t v = sub * WPT + i;
+                    if (v < (uint32_t)W) s_cnt[v * R + d] = acc;
+                    acc += wx[i];
+                }
+            }
+            // old carry -> segment head (only when a line is written; else it stays and grows)
             if (gw > 0) {
                 for (uint32_t x = sub; x < gc; x += TPD) {
-                    s_keys[gS + x] = s_carry[d * G + x];
-                    if constexpr (PAIRS) s_vals[gS + x] = s_cvals[d * G + x];
+                    s_stage[gS + x] = s_stage[CAP + d * G + x];
+                    if constexpr (PAIRS) s_vstage[gS + x] = s_vstage[CAP + d * G + x];
                 }
             }
             // line records
-            const uint32_t nl = (gw + G - 1) / G;
-            for (uint32_t l = sub; l < nl; l += TPD) {
-                const uint32_t lo = l == 0 ? ginv : 0u;
-                s_line[gS / G + l] = make_uint2(gA + l * G, lo | ((uint32_t)G << 8));
+            for (uint32_t l = sub; l * G < gw; l += TPD) s_line[gS / G + l] = (gA + l * G) | (l == 0 ? ginv : 0u);
+            if (leader) {
+                s_lim[d] = gS + gw;
+                if (gw > 0) inv = 0;
+                carry = e - (A + gw);  // pending - written
+                g_run = e;
+                if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
             }
-        }
-        if (leader) {
-            const uint32_t d = d_own;
-#pragma unroll
-            for (int v = 0; v < W; ++v) s_cnt[v * R + d] += S + carry;
-            s_lim[d] = S + wcnt;
-            if (wcnt > 0) inv = 0;
-            carry = carry + (e - g_run) - wcnt;  // pending - written
-            g_run = e;
-            if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
         }
         __syncthreads();
         RS_STAMP(3);
 
-        // ---- 3. rank (lane-ordered returning LDS add) and stage; tails go to the carry
+        // ---- 3. rank (lane-ordered returning LDS add) and stage; tails go to the carry.
+        // Batches of 8 slots: all atomics and limit reads are issued before the first store,
+        // so the LDS round trips overlap instead of serialising slot by slot.
+        constexpr int SB = KPT < 8 ? KPT : 8;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            asm volatile("" : "+v"(key[j]));
-            if (valid == T || (uint32_t)(j * kWave) < plim) {
-                const uint32_t d = dig(key[j]);
-                const uint32_t p = atomicAdd(&s_cnt[w * R + d], 1u);
-                const uint32_t lim = s_lim[d];
-                if (p < lim) {
-                    s_keys[p] = key[j];
-                    if constexpr (PAIRS) s_vals[p] = val[j];
-                } else {
-                    s_carry[d * G + (p - lim)] = key[j];
-                    if constexpr (PAIRS) s_cvals[d * G + (p - lim)] = val[j];
-                }
+        for (int j0 = 0; j0 < KPT; j0 += SB) {
+            uint32_t pp[SB], ll[SB], dd[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
+                dd[u] = dig(key[j]);
+                // padding slots (the grid's last tile only) count into a scratch counter
+                const uint32_t ci = (full || (uint32_t)(j * kWave) < plim) ? w * R + dd[u] : W * R;
+                pp[u] = atomicAdd(&s_cnt[ci], 1u);
+                ll[u] = s_lim[dd[u]];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                uint32_t idx = pp[u] < ll[u] ? pp[u] : CAP + dd[u] * G + (pp[u] - ll[u]);
+                if (!(full || (uint32_t)(j * kWave) < plim)) idx = CAP + R * G;  // scratch slot
+                s_stage[idx] = key[j];
+                if constexpr (PAIRS) s_vstage[idx] = val[j];
             }
         }
         __syncthreads();
         RS_STAMP(4);
-        if (nb < cend) load_tile(nb, key, val);
 
-        // ---- 4. whole lines out: 4 keys per lane
+        // ---- 4. whole lines out: 4 keys per lane (16-B aligned in LDS and in global memory)
         const uint32_t nq = (nseg / G) * QPL;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll 2
         for (uint32_t item = t; item < nq; item += THREADS) {
             const uint32_t L = item / QPL, q = (item % QPL) * 4u;
-            const uint2 rec = s_line[L];
-            const uint32_t lo = rec.y & 0xFFu, hi = rec.y >> 8;
-            const uint4 kv = *reinterpret_cast<const uint4 *>(&s_keys[L * G + q]);
-            uint4 vv;
-            if constexpr (PAIRS) vv = *reinterpret_cast<const uint4 *>(&s_vals[L * G + q]);
-            const uint64_t gp = (uint64_t)rec.x + q;
-            if (lo <= q && q + 4u <= hi) {
-                *reinterpret_cast<uint4 *>(a.kout + gp) = kv;
-                if constexpr (PAIRS) *reinterpret_cast<uint4 *>(a.vout + gp) = vv;
+            const uint32_t rec = s_line[L];
+            const uint32_t lo = rec & (G - 1u);
+            const uint64_t gp = (uint64_t)(rec & ~(G - 1u)) + q;
+            const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
+            u32x4 vv;
+            if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
+            if (lo <= q) {
+                *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
+                if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
             } else {
-                const uint32_t ks[4] = {kv.x, kv.y, kv.z, kv.w};
+                // the chunk's first line: lanes below lo belong to the previous chunk
 #pragma unroll
                 for (uint32_t x = 0; x < 4; ++x)
-                    if (lo <= q + x && q + x < hi) a.kout[gp + x] = ks[x];
-                if constexpr (PAIRS) {
-                    const uint32_t vs[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-                    for (uint32_t x = 0; x < 4; ++x)
-                        if (lo <= q + x && q + x < hi) a.vout[gp + x] = vs[x];
-                }
+                    if (lo <= q + x) {
+                        a.kout[gp + x] = kv[x];
+                        if constexpr (PAIRS) a.vout[gp + x] = vv[x];
+                    }
             }
         }
         RS_STAMP(5);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            key[j] = nkey[j];
+            if constexpr (PAIRS) val[j] = nval[j];
+        }
     }
     // ---- chunk end: the carries (written by the last tile's staging, behind its barrier)
     if (cbeg < cend) {
@@ -936,8 +1000,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             const uint2 fl = s_flush[item / G];
             const uint32_t x = item % G;
             if ((fl.y & 0xFFu) <= x && x < (fl.y >> 8)) {
-                a.kout[(uint64_t)fl.x + x] = s_carry[item];
-                if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_cvals[item];
+                a.kout[(uint64_t)fl.x + x] = s_stage[CAP + item];
+                if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_vstage[CAP + item];
             }
         }
     }
@@ -1004,12 +1068,12 @@ template <int BITS>
 static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
-            rs_histogram<BITS, kHistThreads, kDigitSplit><<<a.num_chunks, kHistThreads, 0, s>>>(a);
+            rs_histogram<BITS, kHistThreads, kDigitSplit><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
             return hipGetLastError();
         }
         return hipErrorInvalidValue;
     }
-    rs_histogram<BITS, kHistThreads, kDigitShift><<<a.num_chunks, kHistThreads, 0, s>>>(a);
+    rs_histogram<BITS, kHistThreads, kDigitShift><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 

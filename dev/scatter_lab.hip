@@ -100,6 +100,7 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
     h.num_chunks = (uint32_t)chunks;
     h.shift = shift;
     h.vec = 1;
+    h.split = 1;
     CK(launch_histogram(BITS, kDigitShift, h, 0));
     ScanArgs s{};
     s.table = c.table;

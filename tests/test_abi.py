@@ -46,9 +46,9 @@ def test_plan_geometry(n, k):
     p = rs.plan(n, k, False, tiles_per_chunk=0)
     assert p.passes == -(-32 // k)
     assert p.bins == 1 << k
-    assert (p.threads, p.tile_keys) in {(256, 4096), (512, 16384), (512, 8192)}
+    assert (p.threads, p.tile_keys) in {(256, 4096), (512, 16384), (512, 8192), (1024, 16384)}
     if n >= 2 * 256 * 16384 and 5 <= k <= 8:
-        assert p.tile_keys == 8192   # whole-line (rs_scatter_lines) tiles for the headline configuration
+        assert (p.threads, p.tile_keys) == (1024, 16384)  # whole-line (rs_scatter_lines) tiles
         assert rs.plan(n, k, True).tile_keys == 16384  # pairs: long digit runs
     assert p.chunk_keys == p.tiles_per_chunk * p.tile_keys
     assert p.num_chunks * p.chunk_keys >= n

@@ -123,9 +123,9 @@ def test_lane_order_probe():
 @pytest.mark.parametrize("dist", ["uniform", "zipf", "allsame", "fewdigits"])
 @pytest.mark.parametrize("tpc", [0, 1, 3, 7])
 def test_whole_line_scatter(dist, tpc):
-    """k = 5..8 keys at n >= 2 * CUs * 8192 run rs_scatter_lines (whole 64-B lines, per-digit
+    """k = 5..8 keys at n >= 2 * CUs * 16384 run rs_scatter_lines (whole 64-B lines, per-digit
     carries across tiles, masked first/last lines per chunk): chunk geometries, skew, ragged n."""
-    n = (1 << 22) + 4099
+    n = (1 << 23) + 4099
     if dist == "uniform":
         x = uniform_keys(n, seed=tpc)
     elif dist == "zipf":
@@ -136,14 +136,14 @@ def test_whole_line_scatter(dist, tpc):
         x = uniform_keys(n, seed=tpc) & np.uint32(0x03030303)
     for k in (8, 5, 7):
         p = rs.plan(n, k, False, tpc)
-        assert p.tile_keys == 8192 and p.threads == 512
+        assert p.tile_keys == 16384 and p.threads == 1024
         assert np.array_equal(gpu_sort(x, k, tiles_per_chunk=tpc), oracle_sort(x, k)), (dist, tpc, k)
 
 
 def test_whole_line_scatter_misaligned_output_falls_back():
     """An output pointer that is 4-B but not 16-B aligned takes the same tiles through
     rs_scatter (no 16-B line stores); the result is the same."""
-    n = (1 << 22) + 77
+    n = (1 << 23) + 77
     x = zipf_keys(n, seed=5)
     big = rs.empty_u32(n + 4)
     for off in (1, 2, 3):

@@ -146,9 +146,24 @@ def test_reference_block_algorithm_breaks_when_k_does_not_divide_32(k):
     the last digit to 32 - bit bits and agrees with Baseline1."""
     n, bs = 4097, 512
     x = zipf_keys(n, seed=bs)
-    y_ref = np.empty_like(x)
-    ref.ref_block_sort(_ptr(x), n, _ptr(y_ref), k, bs)
-    assert not np.array_equal(np.sort(y_ref), np.sort(x))
+    # The defect is undefined behaviour that also writes out of bounds, so the reference runs in
+    # a child process: either it dies (heap corruption) or its output is not a permutation.
+    import subprocess
+    import sys
+    import tempfile
+    from pathlib import Path
+    with tempfile.TemporaryDirectory() as td:
+        xin, yout = Path(td) / "x.npy", Path(td) / "y.npy"
+        np.save(xin, x)
+        code = (
+            "import ctypes, numpy as np, sys; sys.path.insert(0, %r); from _util import ref_lib\n"
+            "x = np.load(%r); y = np.empty_like(x); lib = ref_lib()\n"
+            "lib.ref_block_sort(x.ctypes.data, x.size, y.ctypes.data, %d, %d); np.save(%r, y)\n"
+        ) % (str(Path(__file__).parent), str(xin), k, bs, str(yout))
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=120)
+        if r.returncode == 0:
+            y_ref = np.load(yout)
+            assert not np.array_equal(np.sort(y_ref), np.sort(x))
     lib = __import__("_util").oracle()
     y = np.empty_like(x)
     assert lib.oracle_block_sort(_ptr(x), n, _ptr(y), k, bs) == 0
