@@ -171,7 +171,8 @@ def main():
     scatter_ms = sc["ms"] / max(1, sc["launches"])
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     achieved = bytes_per_key * keys_per_launch / (scatter_ms * 1e-3) / 1e9
-    cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}"
+    kernel = rs.scatter_kernel_name(p) if world == 1 else "rs_scatter"
+    cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel}"
     traffic, traffic_src = traffic_for(cfg_key)
 
     vendor = None
@@ -211,7 +212,7 @@ def main():
                        "pairs": bool(a.pairs), "rank_algo": a.rank, "tile_keys": p.tile_keys,
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
                        "parallelism": "single GPU" if world == 1 else f"range-partition x{world} (RCCL all-to-all)"},
-            "roofline": {"bound": "hbm", "kernel": "rs_scatter (fused local sort + rank + scatter)",
+            "roofline": {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

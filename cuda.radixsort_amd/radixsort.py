@@ -288,6 +288,14 @@ def get_rank_algo() -> int:
     return int(_lib().rsort_get_rank_algo())
 
 
+def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
+    """Which scatter kernel a sort with plan `p` runs (mirrors the dispatch in rsort_kernels.hip)."""
+    if (p.threads, p.tile_keys) == (1024, 16384) and not p.pairs and out_aligned16 \
+            and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
+        return "rs_scatter_lines"
+    return "rs_scatter"
+
+
 def lane_order_probe() -> int:
     """1 if the current device serves same-address LDS atomic lanes in lane order (the default
     ranking then uses one returning LDS add per key), 0 if not (ballot ranking)."""

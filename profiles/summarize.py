@@ -7,8 +7,8 @@ profiles/<tag>_pmc.json: per-kernel FETCH_SIZE / WRITE_SIZE per launch and the H
 scatter launch, corrected as MI355X_MICROARCH.md prescribes for gfx950 and calibrated in-run:
   - FETCH_SIZE counts KiB; on gfx950 it reports half the bytes of a coalesced streaming read.
     Calibration in this run: rs_histogram reads exactly n*4 bytes (16-B loads) -> ratio 0.5.
-  - WRITE_SIZE counts KiB; exact for the dword stores used here. Calibration in this run:
-    rs_gen_uniform writes exactly n*4 bytes with dword stores -> ratio 1.0.
+  - WRITE_SIZE counts KiB; exact for 16-B-per-lane stores (MI355X_MICROARCH.md) and, as
+    calibrated in this run, for dword stores: rs_gen_uniform writes exactly n*4 bytes -> 1.0.
 bench.py reads hbm_bytes_per_launch from this file for roofline.traffic.
 """
 from __future__ import annotations
@@ -58,6 +58,8 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
     read_bytes = sc_fetch * kib / fetch_ratio
     write_bytes = sc_write * kib / write_ratio
     algo = 8.0 * n
+    names = {kn for (kn, c) in list(fetch) + list(write) if "rs_scatter" in kn}
+    kernel = "rs_scatter_lines" if any("rs_scatter_lines" in kn for kn in names) else "rs_scatter"
     rows = {}
     for (kn, c), vs in sorted(fetch.items()) + sorted(write.items()):
         rows.setdefault(kn, {})[c + "_KiB_per_launch"] = sum(vs) / len(vs)
@@ -71,8 +73,9 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
                         "write_ratio_measured": round(write_ratio, 4),
                         "write_ratio_note": "rs_gen_uniform writes exactly 4n bytes with dword stores"},
         "configs": {
-            f"n{n}_k{k}_uniform_keys_match": {
-                "kernel": "rs_scatter (fused local sort + rank + scatter)",
+            f"n{n}_k{k}_uniform_keys_match:{kernel}": {
+                "kernel": f"{kernel} (fused local sort + rank + scatter)",
+                "kernel_symbols": sorted(names),
                 "launches": {"fetch_pass": nf, "write_pass": nw},
                 "read_bytes_per_launch": read_bytes,
                 "write_bytes_per_launch": write_bytes,
