@@ -91,14 +91,14 @@ int device_cus() {
 }
 
 // Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
-// 16384-key tiles (rs_scatter_lines) and pairs use 16384-key tiles (long digit runs); k <= 4 keys
+// 16384-key tiles (rs_scatter_lines), pairs from 8192-key tiles; k <= 4 keys
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
 // CU two large tiles.
 int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
-    if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLarge)) return kGeomLarge;
+    if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     if (k <= 4 && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     return kGeomSmall;
 }
@@ -215,7 +215,7 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     a.nsplit = (uint32_t)nsplit;
     for (int i = 0; i < nsplit; ++i) a.splitters[i] = split[i];
     const int rank = internal_rank((dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH);
-    const int geom = geom_from_shape(p.threads, p.tile_keys);
+    const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
@@ -226,7 +226,7 @@ int check_plan(const rsort_plan *p) {
     if (!p) return RSORT_ERR_ARG;
     if (p->k_bits < kMinBits || p->k_bits > kMaxBits) return RSORT_ERR_BITS;
     if (p->n < 0 || p->n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
-    if (geom_from_shape(p->threads, p->tile_keys) < 0) return RSORT_ERR_ARG;
+    if (geom_from_shape(p->threads, p->tile_keys, p->pairs) < 0) return RSORT_ERR_ARG;
     if (p->tiles_per_chunk <= 0 || p->num_chunks <= 0 ||
         p->num_chunks * p->tiles_per_chunk * p->tile_keys < p->n ||
         p->chunk_keys != p->tiles_per_chunk * p->tile_keys || p->bins != (1 << p->k_bits) ||

@@ -23,17 +23,22 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
 // kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 64-B lines
 // (rs_scatter_lines; one workgroup per CU, its LDS holds the tile plus every digit's carry).
-enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomCount = 4 };
+// kGeomLinesPairs (k = 5..8 pairs): the same with 8192-key tiles of 512 threads (keys + values).
+enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomLinesPairs = 4, kGeomCount = 5 };
 struct GeomShape {
     int threads;
     int kpt;
 };
-constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {512, 16}};
 constexpr int kLineKeys = 16;  // rs_scatter_lines line: 16 keys = 64 B
 inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
-inline int geom_from_shape(int threads, int tile_keys) {
+// K4 and LinesPairs share a shape; pairs (K4 is keys-only) tell them apart.
+inline int geom_from_shape(int threads, int tile_keys, int pairs) {
     for (int g = 0; g < kGeomCount; ++g)
-        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) return g;
+        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) {
+            if (g == kGeomK4 && pairs) return kGeomLinesPairs;
+            return g;
+        }
     return -1;
 }
 

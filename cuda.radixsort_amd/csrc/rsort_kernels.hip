@@ -770,7 +770,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -787,6 +787,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];  // + padding sink
     __shared__ __attribute__((aligned(16))) uint32_t s_vstage[PAIRS ? CAP + R * G + 4 : 4];
     __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
+    __shared__ uint2 s_bl[RF ? W * R : 1];  // RF: per (wave, digit) {LDS base, digit's line limit}
     __shared__ uint32_t s_lim[R];
     __shared__ uint32_t s_line[NL];   // global key index of the line | first valid lane (< G)
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
@@ -853,13 +854,26 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
         for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+        // RF (rank first): the returning add IS the key's rank among its wave's keys of that digit
+        // (lane order, kRankAtomic); two ranks (< 2^16) per register
+        uint32_t rk[RF ? (KPT + 1) / 2 : 1];
         if (full) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+            for (int j = 0; j < KPT; ++j) {
+                if constexpr (RF) {
+                    const uint32_t r = atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                } else {
+                    atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                }
+            }
         } else {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j)
-                if ((uint32_t)(j * kWave) < plim) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+            for (int j = 0; j < KPT; ++j) {
+                uint32_t r = 0;
+                if ((uint32_t)(j * kWave) < plim) r = atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                if constexpr (RF) rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            }
         }
         // next tile's keys: in flight through the scan, staging and output phases
         uint32_t nkey[KPT];
@@ -908,7 +922,10 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 #pragma unroll
                 for (uint32_t i = 0; i < WPT; ++i) {
                     const uint32_t v = sub * WPT + i;
-                    if (v < (uint32_t)W) s_cnt[v * R + d] = acc;
+                    if (v < (uint32_t)W) {
+                        if constexpr (RF) s_bl[v * R + d] = make_uint2(acc, gS + gw);
+                        else s_cnt[v * R + d] = acc;
+                    }
                     acc += wx[i];
                 }
             }
@@ -944,10 +961,16 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 const int j = j0 + u;
                 asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
                 dd[u] = dig(key[j]);
-                // padding slots (the grid's last tile only) count into a scratch counter
-                const uint32_t ci = (full || (uint32_t)(j * kWave) < plim) ? w * R + dd[u] : W * R;
-                pp[u] = atomicAdd(&s_cnt[ci], 1u);
-                ll[u] = s_lim[dd[u]];
+                if constexpr (RF) {
+                    const uint2 bl = s_bl[w * R + dd[u]];
+                    pp[u] = bl.x + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+                    ll[u] = bl.y;
+                } else {
+                    // padding slots (the grid's last tile only) count into a scratch counter
+                    const uint32_t ci = (full || (uint32_t)(j * kWave) < plim) ? w * R + dd[u] : W * R;
+                    pp[u] = atomicAdd(&s_cnt[ci], 1u);
+                    ll[u] = s_lim[dd[u]];
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1110,16 +1133,14 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
     if (geom == kGeomSmall) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
     if constexpr (BITS >= 5 && BITS <= 8) {
         if (geom == kGeomLarge) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLarge>(rank);
-        if constexpr (!PAIRS) {
-            if (geom == kGeomLines) {
-                // whole-line stores need lane-ordered atomics and 16-B aligned outputs; else the
-                // same tiles through rs_scatter
-                if (rank == kRankAtomic && aligned16)
-                    return reinterpret_cast<void *>(
-                        &rs_scatter_lines<BITS, kGeomShape[kGeomLines].threads, kGeomShape[kGeomLines].kpt,
-                                          kLineKeys, false, kDigitShift>);
-                return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLines>(rank);
-            }
+        // whole-line stores need lane-ordered atomics and 16-B aligned outputs; else the same
+        // tiles through rs_scatter
+        constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
+        if (geom == GL) {
+            if (rank == kRankAtomic && aligned16)
+                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
+                                                                  kLineKeys, PAIRS, kDigitShift>);
+            return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }
     if constexpr (BITS <= 4 && !PAIRS) {

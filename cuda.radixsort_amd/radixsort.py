@@ -290,8 +290,9 @@ def get_rank_algo() -> int:
 
 def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
     """Which scatter kernel a sort with plan `p` runs (mirrors the dispatch in rsort_kernels.hip)."""
-    if (p.threads, p.tile_keys) == (1024, 16384) and not p.pairs and out_aligned16 \
-            and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
+    lines = ((p.threads, p.tile_keys) == (1024, 16384) and not p.pairs) or \
+        ((p.threads, p.tile_keys) == (512, 8192) and p.pairs and 5 <= p.k_bits <= 8)
+    if lines and out_aligned16 and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
         return "rs_scatter_lines"
     return "rs_scatter"
 

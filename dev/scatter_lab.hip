@@ -76,10 +76,10 @@ void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps
                                           shift, reps);
 }
 
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true>
 void lines(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
-    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult, rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift>,
-                                          shift, reps);
+    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
+                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF>, shift, reps);
 }
 
 template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
@@ -206,8 +206,10 @@ int main(int argc, char **argv) {
     variant<8, 1024, 24, false, AT, 0, false, 0, 32>(c, "k8 1024x24 atomic wc32", 1.0);
     variant<8, 256, 32, false, AT, 0, false, 0, 32>(c, "k8 256x32 atomic wc32", 1.0);
     variant<8, 512, 16, false, AT, 0, false, 2, 32>(c, "k8 512x16 atomic wc32 nostore", 1.0);
-    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32", 1.0);
+    lines<8, 1024, 16, 32, false, false>(c, "k8 1024x16 lines32", 1.0);
     lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
+    lines<8, 1024, 16, 16, false, false>(c, "k8 1024x16 lines16 cf", 1.0);
+    lines<8, 512, 16, 16, false, false>(c, "k8 512x16 lines16 cf", 1.0);
     lines<8, 512, 16, 32, false>(c, "k8 512x16 lines32", 1.0);
     lines<8, 512, 16, 16, false>(c, "k8 512x16 lines16", 1.0);
     lines<8, 512, 24, 16, false>(c, "k8 512x24 lines16", 1.0);
@@ -224,7 +226,7 @@ int main(int argc, char **argv) {
     variant<8, 512, 32, true, AT, 0>(c, "k8 pairs 512x32 atomic", 1.0);
     variant<8, 512, 16, true, AT, 0>(c, "k8 pairs 512x16 atomic", 1.0);
     variant<8, 512, 16, true, AT, 0, false, 0, 32>(c, "k8 pairs 512x16 atomic wc32", 1.0);
-    lines<8, 1024, 8, 16, true>(c, "k8 pairs 1024x8 lines16", 1.0);
+    lines<8, 1024, 8, 16, true, false>(c, "k8 pairs 1024x8 lines16", 1.0);
     lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
     c.have_ref = false;
     variant<4, 256, 16, false, M, 0>(c, "k4 256x16 match (ref)", 1.0);
