@@ -64,6 +64,62 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
+// Lane-ordered returning LDS add of 1 to cnt[d] for every lane of a full wave (the kRankAtomic
+// premise: same-address lanes are served in lane order, so lane l gets old + #lower lanes with
+// digit d). Same-address lanes serialise in the LDS (about 2 cycles each: 127 cycles when all 64
+// lanes share a counter, dev/lds_rate_lab.hip) and clustered input -- runs of equal keys, as
+// every pass after the first sees for duplicate-heavy data -- does exactly that. So the digit
+// held by lane 0 and the one held by lane 63 (the runs that cross the slot's ends) are added
+// once, by their lowest lane, for all their lanes when they are common (>= 16 lanes); their
+// lanes' ranks come from mbcnt. Uniform data pays two compares and a scalar branch.
+__device__ __forceinline__ uint32_t rank_add(uint32_t *cnt, uint32_t d) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint32_t db = __builtin_amdgcn_readlane(d, kWave - 1);
+    const uint64_t ma = __ballot(d == da);
+    const uint64_t mb = __ballot(d == db);
+    const bool agga = __popcll(ma) >= 16;
+    const bool aggb = da != db && __popcll(mb) >= 16;
+    if (!agga && !aggb) return atomicAdd(&cnt[d], 1u);
+    const uint64_t below = lanes_below();
+    uint32_t r = 0;
+    const bool ina = agga && d == da, inb = aggb && d == db;
+    if (!ina && !inb) r = atomicAdd(&cnt[d], 1u);
+    if (agga) {
+        const uint32_t la = (uint32_t)__builtin_ctzll(ma);
+        uint32_t o = 0;
+        if (lane_id() == la) o = atomicAdd(&cnt[da], (uint32_t)__popcll(ma));
+        o = __builtin_amdgcn_readlane(o, la);
+        if (ina) r = o + (uint32_t)__popcll(ma & below);
+    }
+    if (aggb) {
+        const uint32_t lb = (uint32_t)__builtin_ctzll(mb);
+        uint32_t o = 0;
+        if (lane_id() == lb) o = atomicAdd(&cnt[db], (uint32_t)__popcll(mb));
+        o = __builtin_amdgcn_readlane(o, lb);
+        if (inb) r = o + (uint32_t)__popcll(mb & below);
+    }
+    return r;
+}
+
+// Non-returning form for histograms: lanes sharing lane 0's or lane 63's digit add together.
+// Both forms are exact under any exec mask (inactive lanes take no part in the ballots).
+__device__ __forceinline__ void count_add(uint32_t *cnt, uint32_t d, uint32_t inc = 1u) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint32_t db = __builtin_amdgcn_readlane(d, kWave - 1);
+    const uint64_t ma = __ballot(d == da);
+    const uint64_t mb = __ballot(d == db);
+    const bool agga = __popcll(ma) >= 16;
+    const bool aggb = da != db && __popcll(mb) >= 16;
+    if (!agga && !aggb) {
+        atomicAdd(&cnt[d], inc);
+        return;
+    }
+    const bool ina = agga && d == da, inb = aggb && d == db;
+    if (!ina && !inb) atomicAdd(&cnt[d], inc);
+    if (agga && lane_id() == (uint32_t)__builtin_ctzll(ma)) atomicAdd(&cnt[da], inc * (uint32_t)__popcll(ma));
+    if (aggb && lane_id() == (uint32_t)__builtin_ctzll(mb)) atomicAdd(&cnt[db], inc * (uint32_t)__popcll(mb));
+}
+
 // Mask (lo, hi halves) of the lanes of this wave whose BITS-bit digit equals this lane's:
 // AND over bits b of (ballot(bit b) XNOR my bit b), one v_bitop3 per half per bit
 // (truth table 0x90 = a & ~(b ^ c) with a = mask, b = ballot half, c = my bit as 0 / ~0).
@@ -188,10 +244,25 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (v0 + u * THREADS < nvec) {
-                    atomicAdd(&my[dig(q[u].x)], 1u);
-                    atomicAdd(&my[dig(q[u].y)], 1u);
-                    atomicAdd(&my[dig(q[u].z)], 1u);
-                    atomicAdd(&my[dig(q[u].w)], 1u);
+                    const uint32_t dx = dig(q[u].x), dy = dig(q[u].y), dz = dig(q[u].z), dw = dig(q[u].w);
+                    const bool same4 = dx == dy && dy == dz && dz == dw;
+                    if (__popcll(__ballot(same4)) >= 32) {
+                        // clustered input (runs of equal keys, e.g. duplicates after a pass): one
+                        // add of 4 per lane, lanes sharing the common digits together
+                        if (same4) {
+                            count_add(my, dx, 4u);
+                        } else {
+                            atomicAdd(&my[dx], 1u);
+                            atomicAdd(&my[dy], 1u);
+                            atomicAdd(&my[dz], 1u);
+                            atomicAdd(&my[dw], 1u);
+                        }
+                    } else {
+                        atomicAdd(&my[dx], 1u);
+                        atomicAdd(&my[dy], 1u);
+                        atomicAdd(&my[dz], 1u);
+                        atomicAdd(&my[dw], 1u);
+                    }
                 }
             }
         }
@@ -385,7 +456,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
             // ---- 1. per-wave digit histogram of the tile
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+            for (int j = 0; j < KPT; ++j) count_add(&s_cnt[w * R], dig(key[j]));
             __syncthreads();
             RS_STAMP(2);  // histogram
             // ---- 2. digit scan: s_cnt[w][d] <- tile position of wave w's first key of digit d
@@ -464,7 +535,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                     // base + (#lower lanes with its digit) -- the stable rank, with no ballots.
                     // (verified on every digit width / layout: dev/lds_order_lab.hip; the
                     // library re-checks it per device before selecting this path)
-                    const uint32_t p = atomicAdd(&s_cnt[w * R + d], 1u);
+                    const uint32_t p = rank_add(&s_cnt[w * R], d);
                     s_keys[p] = key[j];
                     if constexpr (PAIRS) s_vals[p] = val[j];
                     continue;
@@ -861,10 +932,10 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 if constexpr (RF) {
-                    const uint32_t r = atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                    const uint32_t r = rank_add(&s_cnt[w * R], dig(key[j]));
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 } else {
-                    atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                    count_add(&s_cnt[w * R], dig(key[j]));
                 }
             }
         } else {
