@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1 << 30)
+    ap.add_argument("--keys", "--n", dest="n", type=int, default=1 << 30, help="keys per GPU")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--pairs", action="store_true")
@@ -106,11 +106,19 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    # RSORT_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on fewer GPUs
+    # (host-side exchange; timings meaningless). The driver's runs use RCCL, one rank per GPU.
+    backend = os.environ.get("RSORT_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
 
     n = a.n

@@ -841,7 +841,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true, int ABL = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -1068,6 +1068,10 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
             u32x4 vv;
             if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
+            if constexpr ((ABL & 2) != 0) {  // dev/scatter_lab ablation: no global stores
+                asm volatile("" ::"v"(kv), "v"(gp));
+                continue;
+            }
             if (lo <= q) {
                 *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
                 if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;

@@ -83,17 +83,31 @@ def choose_splitters(hist: np.ndarray, world: int, top_bits: int) -> list[int]:
     return out
 
 
-def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12, timings=None):
+def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12):
     """Sort the union of every rank's `keys` (and `vals`); return this rank's slice of the
-    global sorted order as (keys, vals, global_offset)."""
+    global sorted order as (keys, vals, global_offset).
+
+    Collectives run on the tensors' device with RCCL ("nccl"); with the gloo backend (tests:
+    several ranks sharing one GPU, or CPU-only ranks) they run on host copies."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if ops is None:
         ops = GpuOps(keys.device)
     dev = keys.device
+    host_comm = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+    cdev = torch.device("cpu") if host_comm else dev
+
+    def a2a(out, inp, out_splits=None, in_splits=None):
+        if not host_comm:
+            dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+            return out
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+        out.copy_(o)
+        return out
 
     # 1-3: global histogram of the top bits -> splitters
-    h = ops.top_histogram(keys, top_bits).to(torch.int64)
+    h = ops.top_histogram(keys, top_bits).to(torch.int64).to(cdev)
     dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
     hist = h.cpu().numpy()
     splitters = choose_splitters(hist, world, top_bits)
@@ -104,7 +118,7 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12, timi
     send = (st[1:] - st[:-1]).astype(np.int64)
 
     # 5: exchange counts
-    send_t = torch.from_numpy(send).to(dev)
+    send_t = torch.from_numpy(send).to(cdev)
     recv_t = torch.empty_like(send_t)
     dist.all_to_all_single(recv_t, send_t, group=group)
     recv = recv_t.cpu().numpy()
@@ -112,19 +126,17 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12, timi
     # 6: exchange keys (and values); chunks arrive in source-rank order (stability)
     n_recv = int(recv.sum())
     rk = torch.empty(n_recv, dtype=keys.dtype, device=dev)
-    dist.all_to_all_single(rk, pk, output_split_sizes=recv.tolist(), input_split_sizes=send.tolist(),
-                           group=group)
+    a2a(rk, pk, recv.tolist(), send.tolist())
     rv = None
     if vals is not None:
         rv = torch.empty(n_recv, dtype=vals.dtype, device=dev)
-        dist.all_to_all_single(rv, pv, output_split_sizes=recv.tolist(), input_split_sizes=send.tolist(),
-                               group=group)
+        a2a(rv, pv, recv.tolist(), send.tolist())
 
     # 7: local LSD sort of the received bucket
     ok, ov = ops.sort(rk, rv, k_bits)
 
     # global offset of this rank's slice = keys owned by lower ranks
-    counts = torch.tensor([n_recv], dtype=torch.int64, device=dev)
+    counts = torch.tensor([n_recv], dtype=torch.int64, device=cdev)
     allc = [torch.zeros_like(counts) for _ in range(world)]
     dist.all_gather(allc, counts, group=group)
     offset = int(sum(int(c.item()) for c in allc[:rank]))

@@ -76,10 +76,11 @@ void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps
                                           shift, reps);
 }
 
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true, int ABL = 0>
 void lines(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
     run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
-                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF>, shift, reps);
+                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF, ABL>, shift,
+                                          reps);
 }
 
 template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
@@ -209,6 +210,9 @@ int main(int argc, char **argv) {
     lines<8, 1024, 16, 32, false, false>(c, "k8 1024x16 lines32", 1.0);
     lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
     lines<8, 1024, 16, 16, false, false>(c, "k8 1024x16 lines16 cf", 1.0);
+    lines<8, 1024, 16, 16, false, true, 2>(c, "k8 1024x16 lines16 nostore", 1.0);
+    lines<8, 512, 32, 16, false>(c, "k8 512x32 lines16", 1.0);
+    lines<8, 512, 32, 16, false, true, 2>(c, "k8 512x32 lines16 nostore", 1.0);
     lines<8, 512, 16, 16, false, false>(c, "k8 512x16 lines16 cf", 1.0);
     lines<8, 512, 16, 32, false>(c, "k8 512x16 lines32", 1.0);
     lines<8, 512, 16, 16, false>(c, "k8 512x16 lines16", 1.0);
