@@ -22,7 +22,7 @@ LIB = PKG / "librsort.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["rsort_kernels.hip", "rsort_capi.cpp", "rsort_vendor.hip"]
+SOURCES = ["rsort_kernels.hip", "rsort_capi.cpp", "rsort_vendor.hip", "rsort_multi.cpp"]
 HEADERS = [CSRC / "rsort_internal.hpp", ROOT / "include" / "rsort.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=hidden",
           f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall"]
@@ -54,7 +54,8 @@ def build(force: bool = False) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or _stale(LIB, objs):
         tmp = LIB.with_suffix(".so.tmp")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
+               "-L/opt/rocm/lib", "-lrccl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)

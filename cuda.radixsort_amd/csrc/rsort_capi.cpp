@@ -366,6 +366,8 @@ const char *rsort_status_string(int status) {
         case RSORT_ERR_HIP: return "HIP runtime error";
         case RSORT_ERR_WORKSPACE: return "workspace too small";
         case RSORT_ERR_NODEV: return "no HIP device";
+        case RSORT_ERR_CAPACITY: return "output capacity too small for the received keys";
+        case RSORT_ERR_COMM: return "RCCL communication error";
         default: return "unknown status";
     }
 }

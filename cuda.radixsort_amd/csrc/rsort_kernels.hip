@@ -1118,6 +1118,11 @@ __global__ void rs_diff_starts(const uint32_t *starts, uint32_t bins, uint32_t *
     if (d < bins) hist[d] = starts[d + 1] - starts[d];
 }
 
+__global__ void rs_widen(const uint32_t *in, unsigned long long *out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1386,6 +1391,12 @@ hipError_t launch_gen_uniform(uint32_t *out, uint64_t n, uint64_t seed, hipStrea
 hipError_t launch_gen_zipf(uint32_t *out, uint64_t n, uint64_t seed, const uint32_t *cdf,
                            uint64_t ranks, hipStream_t s) {
     rs_gen_zipf<<<gen_grid(n), 256, 0, s>>>(out, n, seed, cdf, ranks);
+    return hipGetLastError();
+}
+
+hipError_t launch_widen(const uint32_t *in, unsigned long long *out, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    rs_widen<<<(n + 255) / 256, 256, 0, s>>>(in, out, n);
     return hipGetLastError();
 }
 

@@ -37,7 +37,8 @@ LIB_PATH = PKG / "librsort.so"
 RSORT_OK = 0
 STATUS_NAMES = {0: "RSORT_OK", 1: "RSORT_ERR_ARG", 2: "RSORT_ERR_BITS", 3: "RSORT_ERR_SIZE",
                 4: "RSORT_ERR_ALIGN", 5: "RSORT_ERR_ALLOC", 6: "RSORT_ERR_HIP",
-                7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV"}
+                7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV", 9: "RSORT_ERR_CAPACITY",
+                10: "RSORT_ERR_COMM"}
 RANK_MATCH, RANK_SPLIT, RANK_BALLOT = 0, 1, 2
 PHASES = ("histogram", "scan", "scatter", "copy")
 
@@ -107,6 +108,9 @@ SIGNATURES = {
     "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
     "rsort_partition_device": ([_vp, _vp, _vp, _vp, _i64, _u32p, _int, _vp, _vp, _sz, _vp], _int),
     "rsort_top_histogram": ([_vp, _i64, _int, _vp, _vp, _sz, _vp], _int),
+    "rsort_multi_workspace_size": ([_i64, _i64, _int, _int, _int], _sz),
+    "rsort_u32_multi": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int, _vp,
+                         _vp, _sz, _vp], _int),
     "rsort_vendor_workspace_size": ([_i64], _sz),
     "rsort_u32_vendor_device": ([_vp, _vp, _i64, _vp, _sz, _vp], _int),
     "rsort_u32_vendor": ([_vp, _vp, _i64], _int),
@@ -295,6 +299,68 @@ def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
     if lines and out_aligned16 and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
         return "rs_scatter_lines"
     return "rs_scatter"
+
+
+# ---------------------------------------------------------------- multi-GPU over RCCL (C ABI)
+class NcclUniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]  # NCCL_UNIQUE_ID_BYTES (rccl.h)
+
+
+_rccl = None
+
+
+def _rccl_lib():
+    global _rccl
+    if _rccl is None:
+        _rccl = ctypes.CDLL("librccl.so.1", mode=ctypes.RTLD_GLOBAL)
+        _rccl.ncclGetUniqueId.argtypes = [ctypes.POINTER(NcclUniqueId)]
+        _rccl.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, NcclUniqueId, ctypes.c_int]
+        _rccl.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+    return _rccl
+
+
+def rccl_unique_id() -> bytes:
+    uid = NcclUniqueId()
+    if _rccl_lib().ncclGetUniqueId(ctypes.byref(uid)) != 0:
+        raise RSortError(10, "ncclGetUniqueId")
+    return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))  # raw: the id holds NUL bytes
+
+
+class RcclComm:
+    """An RCCL communicator for rsort_u32_multi (one rank per GPU; the current device)."""
+
+    def __init__(self, world: int, rank: int, uid: bytes):
+        u = NcclUniqueId()
+        if len(uid) != ctypes.sizeof(u):
+            raise ValueError("RCCL unique id must be 128 bytes")
+        ctypes.memmove(ctypes.addressof(u), uid, len(uid))
+        self.handle = ctypes.c_void_p()
+        r = _rccl_lib().ncclCommInitRank(ctypes.byref(self.handle), int(world), u, int(rank))
+        if r != 0:
+            raise RSortError(10, f"ncclCommInitRank (ncclResult {r})")
+        self.world, self.rank = world, rank
+
+    def close(self):
+        if self.handle:
+            _rccl_lib().ncclCommDestroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+def multi_sort_device(comm: RcclComm, keys, k_bits=8, vals=None, capacity=None, stream=None):
+    """rsort_u32_multi: returns (keys_out[:count], vals_out[:count] or None, global offset)."""
+    n = keys.numel()
+    cap = int(capacity if capacity is not None else 2 * n + 4096)
+    pairs = vals is not None
+    kout = empty_u32(cap, keys.device)
+    vout = empty_u32(cap, keys.device) if pairs else None
+    wsb = int(_lib().rsort_multi_workspace_size(n, cap, k_bits, 1 if pairs else 0, comm.world))
+    ws = workspace(wsb, keys.device)
+    cnt, off = ctypes.c_int64(), ctypes.c_int64()
+    _check(_lib().rsort_u32_multi(_ptr(keys), _ptr(vals), n, _ptr(kout), _ptr(vout), cap, ctypes.byref(cnt),
+                                  ctypes.byref(off), int(k_bits), comm.handle, _ptr(ws), wsb, _stream(stream)),
+           "rsort_u32_multi")
+    c = cnt.value
+    return kout[:c], (vout[:c] if pairs else None), off.value
 
 
 def lane_order_probe() -> int:

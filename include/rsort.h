@@ -58,7 +58,9 @@ typedef enum rsort_status {
     RSORT_ERR_ALLOC = 5,      /* hipMalloc / host allocation failed */
     RSORT_ERR_HIP = 6,        /* a HIP runtime call or kernel launch failed */
     RSORT_ERR_WORKSPACE = 7,  /* workspace too small */
-    RSORT_ERR_NODEV = 8       /* no HIP device visible */
+    RSORT_ERR_NODEV = 8,      /* no HIP device visible */
+    RSORT_ERR_CAPACITY = 9,   /* multi-GPU: this rank receives more keys than its output holds */
+    RSORT_ERR_COMM = 10       /* multi-GPU: an RCCL call failed */
 } rsort_status;
 
 /* Local-rank algorithm inside a tile (all give the same, unique, stable result). */
@@ -189,6 +191,23 @@ RSORT_API int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *
 RSORT_API int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits,
                                   uint32_t *d_hist, void *d_workspace, size_t workspace_bytes,
                                   void *stream);
+
+/* ---------------------------------------------------------------- multi-GPU sort (RCCL) */
+/* One rank per GPU over an RCCL communicator (`nccl_comm` is an ncclComm_t; the
+ * reference is single-GPU, Parallel7.cu:10). Every rank passes its n local keys (and values);
+ * on return rank r's d_keys_out[0 .. *out_n) holds the keys of global ranks
+ * [*out_offset, *out_offset + *out_n) of the sorted union, i.e. concatenating the ranks' outputs
+ * in rank order gives Baseline1's result; pairs stay stable (source-rank order). Steps:
+ * top-12-bit histogram -> ncclAllReduce -> splitters -> stable partition into `world` key
+ * ranges -> ncclAllGather of the count matrix -> one grouped ncclSend/ncclRecv exchange ->
+ * local LSD sort. Synchronises `stream` twice (bucket sizes are needed on the host).
+ * capacity: room in d_keys_out / d_vals_out (RSORT_ERR_CAPACITY if exceeded; a balanced input
+ * needs about n). Up to 16 ranks. */
+RSORT_API size_t rsort_multi_workspace_size(int64_t n, int64_t capacity, int k_bits, int pairs, int world);
+RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n,
+                              uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t capacity,
+                              int64_t *out_n, int64_t *out_offset, int k_bits, void *nccl_comm,
+                              void *d_workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------- vendor comparator */
 /* rocPRIM's device radix sort (what sortByThrust resolves to on ROCm), for the

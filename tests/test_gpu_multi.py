@@ -92,3 +92,81 @@ def test_dist_sort_rccl_single_rank():
             assert np.array_equal(rs.to_numpy_u32(ok), rk) and np.array_equal(rs.to_numpy_u32(ov), rv)
         finally:
             dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ C ABI: rsort_u32_multi over RCCL
+def test_c_multi_single_rank():
+    """rsort_u32_multi with a one-rank RCCL communicator: every step (top histogram, all-reduce,
+    partition, all-gather, grouped send/recv, in-place local sort) runs; result = Baseline1."""
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    torch.cuda.set_device(0)
+    comm = rs.RcclComm(1, 0, rs.rccl_unique_id())
+    try:
+        for n, pairs in ((1000003, False), (600001, True), (0, False)):
+            x = zipf_keys(n, seed=n) if n else np.zeros(0, np.uint32)
+            vals = np.arange(n, dtype=np.uint32) if pairs else None
+            ok, ov, off = rs.multi_sort_device(comm, rs.from_numpy_u32(x), 8,
+                                               vals=rs.from_numpy_u32(vals) if pairs else None)
+            torch.cuda.synchronize()
+            assert off == 0 and ok.numel() == n
+            if pairs:
+                rk, rv = oracle_sort_pairs(x, vals, 8)
+                assert np.array_equal(rs.to_numpy_u32(ok), rk) and np.array_equal(rs.to_numpy_u32(ov), rv)
+            else:
+                assert np.array_equal(rs.to_numpy_u32(ok), oracle_sort(x, 8))
+        # capacity too small is reported, not overrun
+        x = uniform_keys(5000)
+        with pytest.raises(rs.RSortError) as e:
+            rs.multi_sort_device(comm, rs.from_numpy_u32(x), 8, capacity=100)
+        assert e.value.status == 9
+    finally:
+        comm.close()
+
+
+def _c_multi_worker(rank, world, uid_path, out_dir, n, pairs):
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    torch.cuda.set_device(0)
+    uid = Path(uid_path).read_bytes()
+    comm = rs.RcclComm(world, rank, uid)
+    try:
+        keys, vals = _inputs(rank, n, "zipf", pairs)
+        ok, ov, off = rs.multi_sort_device(comm, rs.from_numpy_u32(keys), 8,
+                                           vals=rs.from_numpy_u32(vals) if pairs else None)
+        torch.cuda.synchronize()
+        np.save(f"{out_dir}/k{rank}.npy", rs.to_numpy_u32(ok))
+        if pairs:
+            np.save(f"{out_dir}/v{rank}.npy", rs.to_numpy_u32(ov))
+        np.save(f"{out_dir}/o{rank}.npy", np.array([off], np.int64))
+    finally:
+        comm.close()
+
+
+def test_c_multi_two_ranks_one_gpu(tmp_path):
+    """Two RCCL ranks on one GPU (the pool's boxes have one): the exchange logic of the 8-GPU
+    path with real kernels. Skipped if RCCL refuses two ranks on one device."""
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    uid_path = tmp_path / "uid"
+    uid_path.write_bytes(rs.rccl_unique_id())
+    n, world, pairs = 1 << 19, 2, True
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_c_multi_worker, args=(r, world, str(uid_path), str(tmp_path), n, pairs))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    if any(p.exitcode != 0 for p in procs):
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        pytest.skip(f"RCCL with {world} ranks on one GPU unavailable (exit codes {[p.exitcode for p in procs]})")
+    all_k, all_v = zip(*[_inputs(r, n, "zipf", pairs) for r in range(world)])
+    got = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
+    offs = [int(np.load(tmp_path / f"o{r}.npy")[0]) for r in range(world)]
+    assert offs == list(np.cumsum([0] + [g.size for g in got[:-1]]))
+    rk, rv = oracle_sort_pairs(np.concatenate(all_k), np.concatenate(all_v), 8)
+    assert np.array_equal(np.concatenate(got), rk)
+    assert np.array_equal(np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)]), rv)
