@@ -179,7 +179,7 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     // few, long chunks (one scatter workgroup per CU): several histogram workgroups per chunk,
     // their counts added into a zeroed table
     const int cus = device_cus();
-    const int64_t want = 8 * (int64_t)(cus > 0 ? cus : 256);
+    const int64_t want = 4 * (int64_t)(cus > 0 ? cus : 256);  // 1024-thread workgroups (hist_bits)
     a.split = 1;
     if (p.num_chunks < want && p.chunk_keys >= 8 * 4096)
         a.split = (uint32_t)std::min<int64_t>({(want + p.num_chunks - 1) / p.num_chunks, p.chunk_keys / 4096, 64});

@@ -120,6 +120,28 @@ __device__ __forceinline__ void count_add(uint32_t *cnt, uint32_t d, uint32_t in
     if (aggb && lane_id() == (uint32_t)__builtin_ctzll(mb)) atomicAdd(&cnt[db], inc * (uint32_t)__popcll(mb));
 }
 
+// Value of lane (first lane of this lane's aligned group of TPD lanes) + q, for q < TPD: DPP
+// quad permutes (one VALU, no LDS) for groups of up to 4 lanes, ds_bpermute otherwise.
+template <uint32_t TPD>
+__device__ __forceinline__ uint32_t group_lane(uint32_t x, uint32_t q) {
+    if constexpr (TPD == 1) {
+        return x;
+    } else if constexpr (TPD == 2) {
+        // quad_perm (0,0,2,2) / (1,1,3,3)
+        return q == 0 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false)
+                      : (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);
+    } else if constexpr (TPD == 4) {
+        switch (q) {
+            case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);
+            case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x55, 0xF, 0xF, false);
+            case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xAA, 0xF, 0xF, false);
+            default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xFF, 0xF, 0xF, false);
+        }
+    } else {
+        return (uint32_t)__shfl((int)x, (int)((lane_id() & ~(TPD - 1u)) + q));
+    }
+}
+
 // Mask (lo, hi halves) of the lanes of this wave whose BITS-bit digit equals this lane's:
 // AND over bits b of (ballot(bit b) XNOR my bit b), one v_bitop3 per half per bit
 // (truth table 0x90 = a & ~(b ^ c) with a = mask, b = ballot half, c = my bit as 0 / ~0).
@@ -211,7 +233,7 @@ template <int BITS, int THREADS, int DMODE>
 __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
-    constexpr int HW = (R * W <= 2048) ? W : 1;  // per-wave private copies when they fit cheaply
+    constexpr int HW = (R * W <= 4096) ? W : 1;  // per-wave private copies when they fit (<= 16 KB)
     __shared__ uint32_t s_h[HW * R];
 
     const uint32_t t = threadIdx.x;
@@ -971,7 +993,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         uint32_t gpre = 0, cnt = 0;
 #pragma unroll
         for (uint32_t q = 0; q < TPD; ++q) {
-            const uint32_t y = __shfl(part, glead + q);
+            const uint32_t y = group_lane<TPD>(part, q);
             if (q < sub) gpre += y;
             cnt += y;
         }
@@ -983,8 +1005,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         }
         uint32_t nseg;
         const uint32_t S = block_excl_scan1<THREADS>(wcnt, s_ws, nseg);  // next s_ws write is a tile later
-        const uint32_t gS = __shfl(S, glead), gw = __shfl(wcnt, glead);
-        const uint32_t gA = __shfl(A, glead), gc = __shfl(carry, glead), ginv = __shfl(inv, glead);
+        const uint32_t gS = group_lane<TPD>(S, 0), gw = group_lane<TPD>(wcnt, 0);
+        const uint32_t gA = group_lane<TPD>(A, 0), gc = group_lane<TPD>(carry, 0), ginv = group_lane<TPD>(inv, 0);
         {
             const uint32_t d = d_own;
             // per-wave counter bases: after the carry, waves in order
@@ -1002,9 +1024,24 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
             // old carry -> segment head (only when a line is written; else it stays and grows)
             if (gw > 0) {
-                for (uint32_t x = sub; x < gc; x += TPD) {
-                    s_stage[gS + x] = s_stage[CAP + d * G + x];
-                    if constexpr (PAIRS) s_vstage[gS + x] = s_vstage[CAP + d * G + x];
+                // at most (G - 1 + TPD - 1) / TPD slots per thread: all reads, then all writes
+                constexpr uint32_t CPT = (G - 1 + TPD - 1) / TPD;
+                uint32_t ck[CPT], cv[PAIRS ? CPT : 1];
+#pragma unroll
+                for (uint32_t i = 0; i < CPT; ++i) {
+                    const uint32_t x = sub + i * TPD;
+                    if (x < gc) {
+                        ck[i] = s_stage[CAP + d * G + x];
+                        if constexpr (PAIRS) cv[i] = s_vstage[CAP + d * G + x];
+                    }
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < CPT; ++i) {
+                    const uint32_t x = sub + i * TPD;
+                    if (x < gc) {
+                        s_stage[gS + x] = ck[i];
+                        if constexpr (PAIRS) s_vstage[gS + x] = cv[i];
+                    }
                 }
             }
             // line records
@@ -1175,6 +1212,12 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
             return hipGetLastError();
         }
         return hipErrorInvalidValue;
+    }
+    if (a.split > 1) {
+        // few long chunks split over workgroups: 1024-thread workgroups read fastest
+        // (dev/scatter_lab.hip "hist": 6.0 TB/s vs 5.6 TB/s for 256 threads)
+        rs_histogram<BITS, 1024, kDigitShift><<<a.num_chunks * a.split, 1024, 0, s>>>(a);
+        return hipGetLastError();
     }
     rs_histogram<BITS, kHistThreads, kDigitShift><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
     return hipGetLastError();

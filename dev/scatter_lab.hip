@@ -152,6 +152,28 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
     fflush(stdout);
 }
 
+// histogram geometry: THREADS per workgroup, `split` workgroups per chunk, `chunks` chunks
+template <int THREADS>
+void hist_variant(Ctx &c, const char *name, uint32_t chunks, uint32_t split) {
+    if (g_filter && !strstr(name, g_filter)) return;
+    HistArgs h{};
+    h.keys = c.keys;
+    h.table = c.table;
+    h.n = c.n;
+    h.chunk_keys = (c.n + chunks - 1) / chunks;
+    h.chunk_keys = (h.chunk_keys + 16383) / 16384 * 16384;
+    h.num_chunks = chunks;
+    h.shift = 8;
+    h.vec = 1;
+    h.split = split;
+    const float ms = time_ms(c, 5, [&] {
+        hipMemsetAsync(c.table, 0, (size_t)chunks * 256 * 4, 0);
+        rs_histogram<8, THREADS, kDigitShift><<<chunks * split, THREADS>>>(h);
+    });
+    printf("%-34s grid=%-6u %8.3f ms  %7.1f GB/s (read)\n", name, chunks * split, ms, 4.0 * c.n / ms / 1e6);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     Ctx c{};
     const int lg = argc > 1 ? atoi(argv[1]) : 30;
@@ -182,6 +204,13 @@ int main(int argc, char **argv) {
         printf("copy dwordx4 %8.3f ms %7.1f GB/s\n", ms4, 8.0 * c.n / ms4 / 1e6);
         printf("copy dwordx4 (32/CU) %8.3f ms %7.1f GB/s\n", ms4b, 8.0 * c.n / ms4b / 1e6);
     }
+    hist_variant<256>(c, "hist 256 x8", 256, 8);
+    hist_variant<256>(c, "hist 256 x16", 256, 16);
+    hist_variant<256>(c, "hist 256 x32", 256, 32);
+    hist_variant<512>(c, "hist 512 x8", 256, 8);
+    hist_variant<512>(c, "hist 512 x16", 256, 16);
+    hist_variant<1024>(c, "hist 1024 x4", 256, 4);
+    hist_variant<1024>(c, "hist 1024 x8", 256, 8);
     constexpr int M = kRankMatch;
     constexpr int RW = kRankMatchRW;
     constexpr int CT = kRankCount;
