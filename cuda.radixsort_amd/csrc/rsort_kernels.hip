@@ -954,7 +954,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 if constexpr (RF) {
-                    const uint32_t r = rank_add(&s_cnt[w * R], dig(key[j]));
+                    // (ABL & 4: dev/scatter_lab ablation -- plain lane-ordered adds, no aggregation)
+                    const uint32_t r = (ABL & 4) ? atomicAdd(&s_cnt[w * R + dig(key[j])], 1u)
+                                                 : rank_add(&s_cnt[w * R], dig(key[j]));
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 } else {
                     count_add(&s_cnt[w * R], dig(key[j]));

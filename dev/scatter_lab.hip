@@ -240,6 +240,8 @@ int main(int argc, char **argv) {
     lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
     lines<8, 1024, 16, 16, false, false>(c, "k8 1024x16 lines16 cf", 1.0);
     lines<8, 1024, 16, 16, false, true, 2>(c, "k8 1024x16 lines16 nostore", 1.0);
+    lines<8, 1024, 16, 16, false, true, 4>(c, "k8 1024x16 lines16 plainadd", 1.0);
+    lines<8, 1024, 16, 16, false, true, 6>(c, "k8 1024x16 lines16 plainadd nostore", 1.0);
     lines<8, 512, 32, 16, false>(c, "k8 512x32 lines16", 1.0);
     lines<8, 512, 32, 16, false, true, 2>(c, "k8 512x32 lines16 nostore", 1.0);
     lines<8, 512, 16, 16, false, false>(c, "k8 512x16 lines16 cf", 1.0);

@@ -72,6 +72,40 @@ __global__ __launch_bounds__(THREADS) void run_scatter(const uint32_t *__restric
     }
 }
 
+// Same address stream, but written like rs_scatter_lines: each lane stores 16 B (4 keys) with
+// dwordx4 from a 16-B-aligned LDS quad, Q lanes per region run, W16 = 1: 4 lanes per 64-B line.
+template <int THREADS, int KPT>
+__global__ __launch_bounds__(THREADS) void run_scatter_x4(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                          uint64_t n, uint32_t L, uint32_t tpc) {
+    constexpr uint32_t T = THREADS * KPT;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint32_t s[T];
+    const uint32_t R = T / L;
+    const uint64_t region = n / R;
+    const uint64_t cbeg = (uint64_t)blockIdx.x * tpc * T;
+    const uint64_t per_chunk_region = (uint64_t)tpc * L;
+    const uint32_t w = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (uint32_t tile = 0; tile < tpc; ++tile) {
+        const uint64_t tb = cbeg + (uint64_t)tile * T;
+        if (tb + T > n) break;
+        uint32_t k[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = in[tb + w * 64 * KPT + j * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) s[w * 64 * KPT + j * 64 + lane] = k[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT / 4; ++j) {
+            const uint32_t i = (threadIdx.x + j * THREADS) * 4;  // quad start
+            const uint32_t d = i / L;
+            const uint64_t pos = d * region + blockIdx.x * per_chunk_region + (uint64_t)tile * L + (i % L);
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(&s[i]);
+            if (pos + 4 <= n) *reinterpret_cast<u32x4 *>(out + pos) = v;
+        }
+        __syncthreads();
+    }
+}
+
 int main(int argc, char **argv) {
     const int lg = argc > 1 ? atoi(argv[1]) : 30;
     const uint64_t n = 1ull << lg;
@@ -122,6 +156,23 @@ int main(int argc, char **argv) {
             RUN(512, 32, 0, 2, 2);
             RUN(512, 32, 1, 2, 2);
             RUN(512, 32, 1, 3, 2);
+        }
+    }
+    {
+        const uint32_t skew = 0;
+        for (uint32_t L : {64u, 16u, 32u}) {
+            for (int bpc : {1, 2}) {
+                constexpr int TH = 1024, KP = 16;
+                constexpr uint32_t T = TH * KP;
+                const uint64_t tiles = n / T;
+                const uint32_t chunks = cus * bpc;
+                const uint32_t tpc = (uint32_t)((tiles + chunks - 1) / chunks);
+                const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+                char nm[128];
+                snprintf(nm, sizeof nm, "x4 1024x16 L=%-3u aligned bpc=%d", L, bpc);
+                timeit(nm, [&] { run_scatter_x4<TH, KP><<<g, TH>>>(a, b, n, L, tpc); });
+                (void)skew;
+            }
         }
     }
     {
