@@ -64,60 +64,37 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
-// Lane-ordered returning LDS add of 1 to cnt[d] for every lane of a full wave (the kRankAtomic
+// Lane-ordered returning LDS add of 1 to cnt[d] for every lane of a wave (the kRankAtomic
 // premise: same-address lanes are served in lane order, so lane l gets old + #lower lanes with
 // digit d). Same-address lanes serialise in the LDS (about 2 cycles each: 127 cycles when all 64
 // lanes share a counter, dev/lds_rate_lab.hip) and clustered input -- runs of equal keys, as
-// every pass after the first sees for duplicate-heavy data -- does exactly that. So the digit
-// held by lane 0 and the one held by lane 63 (the runs that cross the slot's ends) are added
-// once, by their lowest lane, for all their lanes when they are common (>= 16 lanes); their
-// lanes' ranks come from mbcnt. Uniform data pays two compares and a scalar branch.
+// every pass after the first sees for duplicate-heavy data -- does exactly that. So when the
+// digit held by the first active lane is common (>= 16 lanes: a run crossing the slot's start,
+// or a slot inside one run), it is added once, by that lane, for all its lanes, whose ranks come
+// from mbcnt; a run that starts inside the slot is served lane by lane (once per run). Uniform
+// data pays one compare, a popcount and a scalar branch. Exact under any exec mask.
 __device__ __forceinline__ uint32_t rank_add(uint32_t *cnt, uint32_t d) {
     const uint32_t da = __builtin_amdgcn_readfirstlane(d);
-    const uint32_t db = __builtin_amdgcn_readlane(d, kWave - 1);
     const uint64_t ma = __ballot(d == da);
-    const uint64_t mb = __ballot(d == db);
-    const bool agga = __popcll(ma) >= 16;
-    const bool aggb = da != db && __popcll(mb) >= 16;
-    if (!agga && !aggb) return atomicAdd(&cnt[d], 1u);
-    const uint64_t below = lanes_below();
-    uint32_t r = 0;
-    const bool ina = agga && d == da, inb = aggb && d == db;
-    if (!ina && !inb) r = atomicAdd(&cnt[d], 1u);
-    if (agga) {
-        const uint32_t la = (uint32_t)__builtin_ctzll(ma);
-        uint32_t o = 0;
-        if (lane_id() == la) o = atomicAdd(&cnt[da], (uint32_t)__popcll(ma));
-        o = __builtin_amdgcn_readlane(o, la);
-        if (ina) r = o + (uint32_t)__popcll(ma & below);
-    }
-    if (aggb) {
-        const uint32_t lb = (uint32_t)__builtin_ctzll(mb);
-        uint32_t o = 0;
-        if (lane_id() == lb) o = atomicAdd(&cnt[db], (uint32_t)__popcll(mb));
-        o = __builtin_amdgcn_readlane(o, lb);
-        if (inb) r = o + (uint32_t)__popcll(mb & below);
-    }
-    return r;
+    if (__popcll(ma) < 16) return atomicAdd(&cnt[d], 1u);
+    const uint32_t la = (uint32_t)__builtin_ctzll(ma);
+    uint32_t o = 0;
+    if (d != da) o = atomicAdd(&cnt[d], 1u);
+    if (lane_id() == la) o = atomicAdd(&cnt[da], (uint32_t)__popcll(ma));
+    const uint32_t base = __builtin_amdgcn_readlane(o, la);
+    return d == da ? base + (uint32_t)__popcll(ma & lanes_below()) : o;
 }
 
-// Non-returning form for histograms: lanes sharing lane 0's or lane 63's digit add together.
-// Both forms are exact under any exec mask (inactive lanes take no part in the ballots).
+// Non-returning form for histograms (same aggregation; exact under any exec mask).
 __device__ __forceinline__ void count_add(uint32_t *cnt, uint32_t d, uint32_t inc = 1u) {
     const uint32_t da = __builtin_amdgcn_readfirstlane(d);
-    const uint32_t db = __builtin_amdgcn_readlane(d, kWave - 1);
     const uint64_t ma = __ballot(d == da);
-    const uint64_t mb = __ballot(d == db);
-    const bool agga = __popcll(ma) >= 16;
-    const bool aggb = da != db && __popcll(mb) >= 16;
-    if (!agga && !aggb) {
+    if (__popcll(ma) < 16) {
         atomicAdd(&cnt[d], inc);
         return;
     }
-    const bool ina = agga && d == da, inb = aggb && d == db;
-    if (!ina && !inb) atomicAdd(&cnt[d], inc);
-    if (agga && lane_id() == (uint32_t)__builtin_ctzll(ma)) atomicAdd(&cnt[da], inc * (uint32_t)__popcll(ma));
-    if (aggb && lane_id() == (uint32_t)__builtin_ctzll(mb)) atomicAdd(&cnt[db], inc * (uint32_t)__popcll(mb));
+    if (d != da) atomicAdd(&cnt[d], inc);
+    if (lane_id() == (uint32_t)__builtin_ctzll(ma)) atomicAdd(&cnt[da], inc * (uint32_t)__popcll(ma));
 }
 
 // Value of lane (first lane of this lane's aligned group of TPD lanes) + q, for q < TPD: DPP
