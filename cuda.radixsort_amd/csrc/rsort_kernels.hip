@@ -859,7 +859,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
     __shared__ uint2 s_bl[RF ? W * R : 1];  // RF: per (wave, digit) {LDS base, digit's line limit}
     __shared__ uint32_t s_lim[R];
-    __shared__ uint32_t s_line[NL];   // global key index of the line | first valid lane (< G)
+    __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
 
@@ -882,6 +882,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         carry = g & (G - 1u);  // the first line starts before the chunk's output
         inv = carry;
         g_run = g;
+        // the invalid slots get a key of this digit (never stored: masked), so every staged
+        // slot's key tells the output phase its digit
+        for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = d_own << a.shift;
     }
 
     const uint32_t base = w * SEG + lane;
@@ -1023,9 +1026,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                     }
                 }
             }
-            // line records
-            for (uint32_t l = sub; l * G < gw; l += TPD) s_line[gS / G + l] = (gA + l * G) | (l == 0 ? ginv : 0u);
             if (leader) {
+                s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
                 s_lim[d] = gS + gw;
                 if (gw > 0) inv = 0;
                 carry = e - (A + gw);  // pending - written
@@ -1078,10 +1080,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 #pragma unroll 2
         for (uint32_t item = t; item < nq; item += THREADS) {
             const uint32_t L = item / QPL, q = (item % QPL) * 4u;
-            const uint32_t rec = s_line[L];
-            const uint32_t lo = rec & (G - 1u);
-            const uint64_t gp = (uint64_t)(rec & ~(G - 1u)) + q;
+            // every key of an LDS line has the line's digit: it locates the line's segment
             const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
+            const uint2 info = s_out[dig(kv.x)];
+            const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
+            const uint64_t gp = (uint64_t)(info.x + L * G + q);
             u32x4 vv;
             if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
             if constexpr ((ABL & 2) != 0) {  // dev/scatter_lab ablation: no global stores
