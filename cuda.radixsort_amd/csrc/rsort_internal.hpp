@@ -21,16 +21,20 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // (dev/scatter_lab): the digit runs a tile writes must be long enough to fill 128-B lines, so
 // k = 5..8 uses 16384-key tiles; k <= 4 has long runs already; k >= 9 and small inputs use
 // 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
-// kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 64-B lines
+// kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 128-B lines
 // (rs_scatter_lines; one workgroup per CU, its LDS holds the tile plus every digit's carry).
-// kGeomLinesPairs (k = 5..8 pairs): the same with 8192-key tiles of 512 threads (keys + values).
+// kGeomLinesPairs (k = 5..8 pairs): 8192-key tiles of 512 threads (keys + values), 64-B lines.
 enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomLinesPairs = 4, kGeomCount = 5 };
 struct GeomShape {
     int threads;
     int kpt;
 };
 constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {512, 16}};
-constexpr int kLineKeys = 16;  // rs_scatter_lines line: 16 keys = 64 B
+// rs_scatter_lines line width. Keys-only stages whole 128-B lines (the L2 line: runs that start or
+// end mid-line cost about a third more HBM time, dev/runlen_lab.hip); pairs keep 64-B lines (two
+// 128-B carry areas do not fit in LDS beside 8192-key tiles of keys and values).
+constexpr int kLineKeys = 32;
+constexpr int kLineKeysPairs = 16;
 inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
 // K4 and LinesPairs share a shape; pairs (K4 is keys-only) tell them apart.
 inline int geom_from_shape(int threads, int tile_keys, int pairs) {

@@ -850,15 +850,16 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t CAP = T + (G - 1) * R;        // staged keys incl. carries, worst case
     constexpr uint32_t NL = CAP / G;
     constexpr uint32_t QPL = G / 4;                  // 16-B quads per line
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     static_assert(R <= THREADS && TPD <= kWave && (G == 16 || G == 32),
                   "a digit's thread group lies in one wave; 64/128-B lines");
+    static_assert(CAP + R * G < 65536u, "LDS slot indices are packed in 16 bits");
 
     // staging: [0, CAP) whole lines of every digit, [CAP, CAP + R*G) the per-digit carries
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];  // + padding sink
     __shared__ __attribute__((aligned(16))) uint32_t s_vstage[PAIRS ? CAP + R * G + 4 : 4];
     __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
-    __shared__ uint2 s_bl[RF ? W * R : 1];  // RF: per (wave, digit) {LDS base, digit's line limit}
-    __shared__ uint32_t s_lim[R];
+    __shared__ uint32_t s_lim[RF ? 1 : R];  // !RF: per digit, the LDS index past its last whole line
     __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
@@ -911,6 +912,34 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         }
     };
 
+    // step 4's unit of work: one 16-B quad of a staged whole line -> global (4 lanes per line)
+    auto out_quad = [&](uint32_t item) {
+        const uint32_t L = item / QPL, q = (item % QPL) * 4u;
+        // every key of an LDS line has the line's digit: it locates the line's segment
+        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
+        const uint2 info = s_out[dig(kv.x)];
+        const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
+        const uint64_t gp = (uint64_t)(info.x + L * G + q);
+        u32x4 vv;
+        if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
+        if constexpr ((ABL & 2) != 0) {  // dev/scatter_lab ablation: no global stores
+            asm volatile("" ::"v"(kv), "v"(gp));
+            return;
+        }
+        if (lo <= q) {
+            *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
+            if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
+        } else {
+            // the chunk's first line: lanes below lo belong to the previous chunk
+#pragma unroll
+            for (uint32_t x = 0; x < 4; ++x)
+                if (lo <= q + x) {
+                    a.kout[gp + x] = kv[x];
+                    if constexpr (PAIRS) a.vout[gp + x] = vv[x];
+                }
+        }
+    };
+
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
@@ -930,6 +959,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         // RF (rank first): the returning add IS the key's rank among its wave's keys of that digit
         // (lane order, kRankAtomic); two ranks (< 2^16) per register
         uint32_t rk[RF ? (KPT + 1) / 2 : 1];
+        uint32_t nkey[KPT];
+        uint32_t nval[PAIRS ? KPT : 1];
         if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
@@ -945,14 +976,13 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         } else {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = dig(key[j]);
                 uint32_t r = 0;
-                if ((uint32_t)(j * kWave) < plim) r = atomicAdd(&s_cnt[w * R + dig(key[j])], 1u);
+                if ((uint32_t)(j * kWave) < plim) r = atomicAdd(&s_cnt[w * R + d], 1u);
                 if constexpr (RF) rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         }
         // next tile's keys: in flight through the scan, staging and output phases
-        uint32_t nkey[KPT];
-        uint32_t nval[PAIRS ? KPT : 1];
         if (nb < cend) load_tile(nb, nkey, nval);
         __syncthreads();
         RS_STAMP(2);
@@ -980,6 +1010,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             cnt += y;
         }
         uint32_t wcnt = 0, A = 0, e = 0;
+        RS_STAMP(1);
         if (leader) {
             A = g_run - carry;  // line-aligned
             e = g_run + cnt;
@@ -987,6 +1018,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         }
         uint32_t nseg;
         const uint32_t S = block_excl_scan1<THREADS>(wcnt, s_ws, nseg);  // next s_ws write is a tile later
+        RS_STAMP(3);
         const uint32_t gS = group_lane<TPD>(S, 0), gw = group_lane<TPD>(wcnt, 0);
         const uint32_t gA = group_lane<TPD>(A, 0), gc = group_lane<TPD>(carry, 0), ginv = group_lane<TPD>(inv, 0);
         {
@@ -998,14 +1030,44 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 for (uint32_t i = 0; i < WPT; ++i) {
                     const uint32_t v = sub * WPT + i;
                     if (v < (uint32_t)W) {
-                        if constexpr (RF) s_bl[v * R + d] = make_uint2(acc, gS + gw);
+                        // RF: {LDS base | the digit's line limit << 16} (both < CAP < 2^16), read
+                        // back with one ds_read_b32 per key in step 3
+                        if constexpr (RF) s_cnt[v * R + d] = acc | ((gS + gw) << 16);
                         else s_cnt[v * R + d] = acc;
                     }
                     acc += wx[i];
                 }
             }
             // old carry -> segment head (only when a line is written; else it stays and grows)
-            if (gw > 0) {
+            constexpr uint32_t CB = G / TPD;  // contiguous carry slots per group thread
+            if constexpr (G % TPD == 0 && CB % 4 == 0) {
+                // each thread moves its CB slots as 16-B quads (the carry area and the segment
+                // head are both line-aligned); only the quad holding the carry's end is split
+                const uint32_t x0 = sub * CB;
+                if (gw > 0 && x0 < gc) {
+                    u32x4 ck[CB / 4], cv[PAIRS ? CB / 4 : 1];
+#pragma unroll
+                    for (uint32_t i = 0; i < CB / 4; ++i) {
+                        ck[i] = *reinterpret_cast<const u32x4 *>(&s_stage[CAP + d * G + x0 + 4 * i]);
+                        if constexpr (PAIRS) cv[i] = *reinterpret_cast<const u32x4 *>(&s_vstage[CAP + d * G + x0 + 4 * i]);
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < CB / 4; ++i) {
+                        const uint32_t x = x0 + 4 * i;
+                        if (x + 4 <= gc) {
+                            *reinterpret_cast<u32x4 *>(&s_stage[gS + x]) = ck[i];
+                            if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(&s_vstage[gS + x]) = cv[i];
+                        } else if (x < gc) {
+#pragma unroll
+                            for (uint32_t e = 0; e < 4; ++e)
+                                if (x + e < gc) {
+                                    s_stage[gS + x + e] = ck[i][e];
+                                    if constexpr (PAIRS) s_vstage[gS + x + e] = cv[i][e];
+                                }
+                        }
+                    }
+                }
+            } else if (gw > 0) {
                 // at most (G - 1 + TPD - 1) / TPD slots per thread: all reads, then all writes
                 constexpr uint32_t CPT = (G - 1 + TPD - 1) / TPD;
                 uint32_t ck[CPT], cv[PAIRS ? CPT : 1];
@@ -1028,20 +1090,22 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
             if (leader) {
                 s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
-                s_lim[d] = gS + gw;
+                if constexpr (!RF) s_lim[d] = gS + gw;
                 if (gw > 0) inv = 0;
                 carry = e - (A + gw);  // pending - written
                 g_run = e;
                 if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
             }
         }
+        RS_STAMP(4);
         __syncthreads();
-        RS_STAMP(3);
+        RS_STAMP(5);
 
         // ---- 3. rank (lane-ordered returning LDS add) and stage; tails go to the carry.
         // Batches of 8 slots: all atomics and limit reads are issued before the first store,
         // so the LDS round trips overlap instead of serialising slot by slot.
         constexpr int SB = KPT < 8 ? KPT : 8;
+        static_assert(KPT % SB == 0, "whole batches of slots");
 #pragma unroll
         for (int j0 = 0; j0 < KPT; j0 += SB) {
             uint32_t pp[SB], ll[SB], dd[SB];
@@ -1051,9 +1115,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
                 dd[u] = dig(key[j]);
                 if constexpr (RF) {
-                    const uint2 bl = s_bl[w * R + dd[u]];
-                    pp[u] = bl.x + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
-                    ll[u] = bl.y;
+                    const uint32_t bl = s_cnt[w * R + dd[u]];
+                    pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+                    ll[u] = bl >> 16;
                 } else {
                     // padding slots (the grid's last tile only) count into a scratch counter
                     const uint32_t ci = (full || (uint32_t)(j * kWave) < plim) ? w * R + dd[u] : W * R;
@@ -1072,39 +1136,13 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
         }
         __syncthreads();
-        RS_STAMP(4);
+        RS_STAMP(6);
 
         // ---- 4. whole lines out: 4 keys per lane (16-B aligned in LDS and in global memory)
         const uint32_t nq = (nseg / G) * QPL;
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll 2
-        for (uint32_t item = t; item < nq; item += THREADS) {
-            const uint32_t L = item / QPL, q = (item % QPL) * 4u;
-            // every key of an LDS line has the line's digit: it locates the line's segment
-            const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
-            const uint2 info = s_out[dig(kv.x)];
-            const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
-            const uint64_t gp = (uint64_t)(info.x + L * G + q);
-            u32x4 vv;
-            if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
-            if constexpr ((ABL & 2) != 0) {  // dev/scatter_lab ablation: no global stores
-                asm volatile("" ::"v"(kv), "v"(gp));
-                continue;
-            }
-            if (lo <= q) {
-                *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
-                if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
-            } else {
-                // the chunk's first line: lanes below lo belong to the previous chunk
-#pragma unroll
-                for (uint32_t x = 0; x < 4; ++x)
-                    if (lo <= q + x) {
-                        a.kout[gp + x] = kv[x];
-                        if constexpr (PAIRS) a.vout[gp + x] = vv[x];
-                    }
-            }
-        }
-        RS_STAMP(5);
+        for (uint32_t item = t; item < nq; item += THREADS) out_quad(item);
+        RS_STAMP(7);
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             key[j] = nkey[j];
@@ -1205,6 +1243,7 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifndef RSORT_LAB_LITE  // dev labs that instantiate their own variants skip the library's set
 // The compiled scatter kernels. "match" (the default rank algorithm) is the count-first peer
 // match (kRankCount); "split" is the reference's 1-bit split sort. Geometries per kGeomShape.
 template <int BITS, bool PAIRS, int RANK, int DMODE, int G>
@@ -1244,7 +1283,8 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         if (geom == GL) {
             if (rank == kRankAtomic && aligned16)
                 return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
-                                                                  kLineKeys, PAIRS, kDigitShift>);
+                                                                  PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
+                                                                  kDigitShift>);
             return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }
@@ -1277,6 +1317,8 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
         default: return nullptr;
     }
 }
+
+#endif  // RSORT_LAB_LITE
 
 // ------------------------------------------------------------------------------ lane-order probe
 // Every lane of a wave adds to one of a few LDS counters with a returning atomic and checks the
@@ -1358,6 +1400,7 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
     }
 }
 
+#ifndef RSORT_LAB_LITE
 bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom) {
     if (geom < 0 || geom >= kGeomCount) return false;
     return scatter_kernel(bits, pairs, rank_algo, dmode, geom, 1) != nullptr;
@@ -1382,6 +1425,8 @@ int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom) {
         return 0;
     return nb;
 }
+
+#endif  // RSORT_LAB_LITE
 
 hipError_t launch_scan(const ScanArgs &a, hipStream_t s) {
     rs_scan_reduce<<<a.nblocks, kScanThreads, 0, s>>>(a);

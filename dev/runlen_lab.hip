@@ -1,0 +1,107 @@
+// runlen_lab.hip -- development harness: HBM cost of an LSD-scatter-shaped write stream as a
+// function of the run length. A persistent grid walks chunks of 16384-key tiles; each tile is read
+// with coalesced 16-B loads and written as T/L runs of L keys (16-B stores, whole aligned lines),
+// run r of every tile continuing region r where the same chunk's previous tile stopped -- the
+// address stream of a pass whose digit runs are L keys long. Same bytes for every L.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 dev/runlen_lab.hip -o dev/runlen_lab
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            printf("HIP error %s at line %d\n", hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int THREADS, int QPT>
+__global__ __launch_bounds__(THREADS) void runs(const u32x4 *__restrict__ in, uint32_t *__restrict__ out, uint64_t n,
+                                                 uint32_t L, uint32_t tpc, uint32_t skew) {
+    constexpr uint32_t T = THREADS * QPT * 4;
+    const uint32_t R = T / L;
+    const uint64_t region = n / R - 32;
+    const uint64_t cbeg = (uint64_t)blockIdx.x * tpc * T;
+    for (uint32_t tile = 0; tile < tpc; ++tile) {
+        const uint64_t tb = cbeg + (uint64_t)tile * T;
+        if (tb + T > n) break;
+        u32x4 v[QPT];
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) v[j] = in[tb / 4 + threadIdx.x + j * THREADS];
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const uint32_t i = (threadIdx.x + j * THREADS) * 4;
+            const uint32_t r = i / L;
+            // skew: every region (and so every run) starts `skew` keys past a 128-B boundary
+            const uint64_t pos = r * region + skew + (uint64_t)blockIdx.x * tpc * L + (uint64_t)tile * L + (i % L);
+            *reinterpret_cast<u32x4 *>(out + pos) = v[j];
+        }
+    }
+}
+
+template <int THREADS, int QPT>
+__global__ __launch_bounds__(THREADS) void copy(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, uint64_t n4) {
+    for (uint64_t b = (uint64_t)blockIdx.x * THREADS * QPT; b < n4; b += (uint64_t)gridDim.x * THREADS * QPT) {
+        u32x4 v[QPT];
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) v[j] = in[b + threadIdx.x + j * THREADS];
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) out[b + threadIdx.x + j * THREADS] = v[j];
+    }
+}
+
+int main(int argc, char **argv) {
+    const int lg = argc > 1 ? atoi(argv[1]) : 30;
+    const uint64_t n = 1ull << lg;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    uint32_t *a, *b;
+    CK(hipMalloc(&a, n * 4));
+    CK(hipMalloc(&b, n * 4));
+    CK(hipMemset(a, 1, n * 4));
+    CK(hipMemset(b, 2, n * 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char *name, auto f) {
+        f();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        const int reps = 10;
+        for (int i = 0; i < reps; ++i) f();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipGetLastError());
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= reps;
+        printf("%-48s %8.3f ms %8.1f GB/s\n", name, ms, 8.0 * n / ms / 1e6);
+        fflush(stdout);
+    };
+    char nm[128];
+    for (int g : {1, 2, 4}) {
+        snprintf(nm, sizeof nm, "copy 256x4q grid=%d/CU", g);
+        timeit(nm, [&] { copy<256, 4><<<cus * g, 256>>>((const u32x4 *)a, (u32x4 *)b, n / 4); });
+        snprintf(nm, sizeof nm, "copy 1024x4q grid=%d/CU", g);
+        timeit(nm, [&] { copy<1024, 4><<<cus * g, 1024>>>((const u32x4 *)a, (u32x4 *)b, n / 4); });
+    }
+    for (uint32_t L : {32u, 64u, 128u}) {
+        for (uint32_t skew : {0u, 16u, 8u, 4u}) {
+            constexpr int TH = 1024, Q = 4;
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t chunks = cus;
+            const uint32_t tpc = (uint32_t)((tiles + chunks - 1) / chunks);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            snprintf(nm, sizeof nm, "runs 1024x16 L=%-4u (%4u B) skew=%-2u keys", L, L * 4, skew);
+            timeit(nm, [&] { runs<TH, Q><<<g, TH>>>((const u32x4 *)a, b, n, L, tpc, skew); });
+        }
+    }
+    return 0;
+}

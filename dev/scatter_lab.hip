@@ -4,6 +4,9 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc \
 //         dev/scatter_lab.hip -o dev/scatter_lab && dev/scatter_lab [log2n]
+#ifdef LINES_ONLY
+#define RSORT_LAB_LITE
+#endif
 #include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
 
 #include <stdio.h>
@@ -143,9 +146,9 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
         for (uint64_t b = 0; b < chunks; ++b)
             for (int i = 0; i < 8; ++i) sum[i] += st[b * 8 + i];
         for (int i = 0; i < 8; ++i) tot += sum[i];
-        const char *names[8] = {"wait-keys", "reset+bar", "rank", "scan", "stage", "output", "-", "-"};
+        const char *names[8] = {"wait-keys", "2a:cnt-reads", "1:rank+bar", "2b:scan", "2c:bases+carry", "2d:bar", "3:stage+bar", "4:output"};
         printf("    stamps per tile (cycles, wave 0):");
-        for (int i = 0; i < 6; ++i) printf(" %s=%.0f (%.0f%%)", names[i], sum[i] / chunks / tpc, 100.0 * sum[i] / tot);
+        for (int i = 0; i < 8; ++i) printf(" %s=%.0f (%.0f%%)", names[i], sum[i] / chunks / tpc, 100.0 * sum[i] / tot);
         printf("\n");
     }
 #endif
@@ -204,6 +207,17 @@ int main(int argc, char **argv) {
         printf("copy dwordx4 %8.3f ms %7.1f GB/s\n", ms4, 8.0 * c.n / ms4 / 1e6);
         printf("copy dwordx4 (32/CU) %8.3f ms %7.1f GB/s\n", ms4b, 8.0 * c.n / ms4b / 1e6);
     }
+#ifdef LINES_ONLY
+    // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
+    lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
+    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32", 1.0);
+    lines<8, 1024, 16, 32, false, true, 2>(c, "k8 1024x16 lines32 nostore", 1.0);
+    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32 again", 1.0);
+    c.have_ref = false;
+    lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
+    lines<8, 1024, 8, 16, true>(c, "k8 pairs 1024x8 lines16", 1.0);
+    return 0;
+#endif
     hist_variant<256>(c, "hist 256 x8", 256, 8);
     hist_variant<256>(c, "hist 256 x16", 256, 16);
     hist_variant<256>(c, "hist 256 x32", 256, 32);
