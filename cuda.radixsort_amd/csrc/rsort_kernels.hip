@@ -206,7 +206,7 @@ struct Digit {
 
 // ------------------------------------------------------------------------------ histogram
 // Reference: histogramKernel (Parallel7.cu:318-343) + transpose (P7:361-392, :596).
-template <int BITS, int THREADS, int DMODE>
+template <int BITS, int THREADS, int DMODE, int NT = 0>
 __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -230,15 +230,17 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     const uint64_t end = min(beg + part, cend);
     uint64_t tail = beg;
     if (a.vec) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(a.keys + beg);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
         const uint32_t nvec = (uint32_t)((end - beg) / 4);
         constexpr int U = 4;
         for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
-            uint4 q[U];
+            u32x4 q[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t v = v0 + u * THREADS;
-                q[u] = v < nvec ? p[v] : make_uint4(0, 0, 0, 0);
+                // NT: non-temporal loads (the keys are read once per pass)
+                q[u] = v < nvec ? (NT ? __builtin_nontemporal_load(p + v) : p[v]) : u32x4{0, 0, 0, 0};
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -840,7 +842,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true, int ABL = 0>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true, int ABL = 0, int NT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -898,8 +900,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         if (valid == T) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                k[j] = tk[j * kWave];
-                if constexpr (PAIRS) v[j] = tv[j * kWave];
+                // NT & 1: non-temporal key/value loads (dev/scatter_lab experiment)
+                k[j] = (NT & 1) ? __builtin_nontemporal_load(tk + j * kWave) : tk[j * kWave];
+                if constexpr (PAIRS) v[j] = (NT & 1) ? __builtin_nontemporal_load(tv + j * kWave) : tv[j * kWave];
             }
         } else {
             const uint32_t lim = valid > lb ? valid - lb : 0u;
@@ -927,8 +930,13 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             return;
         }
         if (lo <= q) {
-            *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
-            if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
+            if constexpr ((NT & 2) != 0) {  // non-temporal whole-line stores (dev/scatter_lab experiment)
+                __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
+                if constexpr (PAIRS) __builtin_nontemporal_store(vv, reinterpret_cast<u32x4 *>(a.vout + gp));
+            } else {
+                *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
+                if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
+            }
         } else {
             // the chunk's first line: lanes below lo belong to the previous chunk
 #pragma unroll
@@ -1228,7 +1236,7 @@ template <int BITS>
 static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
-            rs_histogram<BITS, kHistThreads, kDigitSplit><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
+            rs_histogram<BITS, kHistThreads, kDigitSplit, 1><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
             return hipGetLastError();
         }
         return hipErrorInvalidValue;
@@ -1236,10 +1244,11 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (a.split > 1) {
         // few long chunks split over workgroups: 1024-thread workgroups read fastest
         // (dev/scatter_lab.hip "hist": 6.0 TB/s vs 5.6 TB/s for 256 threads)
-        rs_histogram<BITS, 1024, kDigitShift><<<a.num_chunks * a.split, 1024, 0, s>>>(a);
+        // non-temporal 16-B loads: 6.8 TB/s vs 6.1 TB/s (dev/scatter_lab.hip "hist ... nt")
+        rs_histogram<BITS, 1024, kDigitShift, 1><<<a.num_chunks * a.split, 1024, 0, s>>>(a);
         return hipGetLastError();
     }
-    rs_histogram<BITS, kHistThreads, kDigitShift><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
+    rs_histogram<BITS, kHistThreads, kDigitShift, 1><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
@@ -1284,7 +1293,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
             if (rank == kRankAtomic && aligned16)
                 return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
                                                                   PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
-                                                                  kDigitShift>);
+                                                                  kDigitShift, true, 0, PAIRS ? 0 : 3>);
             return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }

@@ -79,10 +79,10 @@ void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps
                                           shift, reps);
 }
 
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true, int ABL = 0>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true, int ABL = 0, int NT = 0>
 void lines(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
     run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
-                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF, ABL>, shift,
+                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF, ABL, NT>, shift,
                                           reps);
 }
 
@@ -156,7 +156,7 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
 }
 
 // histogram geometry: THREADS per workgroup, `split` workgroups per chunk, `chunks` chunks
-template <int THREADS>
+template <int THREADS, int NT = 0>
 void hist_variant(Ctx &c, const char *name, uint32_t chunks, uint32_t split) {
     if (g_filter && !strstr(name, g_filter)) return;
     HistArgs h{};
@@ -171,7 +171,7 @@ void hist_variant(Ctx &c, const char *name, uint32_t chunks, uint32_t split) {
     h.split = split;
     const float ms = time_ms(c, 5, [&] {
         hipMemsetAsync(c.table, 0, (size_t)chunks * 256 * 4, 0);
-        rs_histogram<8, THREADS, kDigitShift><<<chunks * split, THREADS>>>(h);
+        rs_histogram<8, THREADS, kDigitShift, NT><<<chunks * split, THREADS>>>(h);
     });
     printf("%-34s grid=%-6u %8.3f ms  %7.1f GB/s (read)\n", name, chunks * split, ms, 4.0 * c.n / ms / 1e6);
     fflush(stdout);
@@ -209,13 +209,19 @@ int main(int argc, char **argv) {
     }
 #ifdef LINES_ONLY
     // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
-    lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
+    hist_variant<1024>(c, "hist 1024 x4", 256, 4);
+    hist_variant<1024, 1>(c, "hist 1024 x4 nt", 256, 4);
+    hist_variant<1024>(c, "hist 1024 x8", 256, 8);
+    hist_variant<1024, 1>(c, "hist 1024 x8 nt", 256, 8);
+    hist_variant<512, 1>(c, "hist 512 x8 nt", 256, 8);
+    hist_variant<1024, 1>(c, "hist 1024 x2 nt", 256, 2);
     lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32", 1.0);
-    lines<8, 1024, 16, 32, false, true, 2>(c, "k8 1024x16 lines32 nostore", 1.0);
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 ntboth", 1.0);
     lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32 again", 1.0);
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 ntboth again", 1.0);
     c.have_ref = false;
     lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
-    lines<8, 1024, 8, 16, true>(c, "k8 pairs 1024x8 lines16", 1.0);
+    lines<8, 512, 16, 16, true, true, 0, 3>(c, "k8 pairs 512x16 lines16 ntboth", 1.0);
     return 0;
 #endif
     hist_variant<256>(c, "hist 256 x8", 256, 8);
