@@ -13,6 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <math.h>
+
 #include <vector>
 
 using namespace rsort;
@@ -150,13 +152,26 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
         printf("    stamps per tile (cycles, wave 0):");
         for (int i = 0; i < 8; ++i) printf(" %s=%.0f (%.0f%%)", names[i], sum[i] / chunks / tpc, 100.0 * sum[i] / tot);
         printf("\n");
+        // per-chunk totals: the slowest workgroup sets the kernel time
+        double mn = 1e30, mx = 0;
+        uint64_t bmx = 0;
+        for (uint64_t b = 0; b < chunks; ++b) {
+            double tb = 0;
+            for (int i = 0; i < 8; ++i) tb += st[b * 8 + i];
+            if (tb < mn) mn = tb;
+            if (tb > mx) { mx = tb; bmx = b; }
+        }
+        printf("    per-chunk cycles: min=%.0f avg=%.0f max=%.0f (chunk %llu:", mn, tot / chunks, mx,
+               (unsigned long long)bmx);
+        for (int i = 0; i < 8; ++i) printf(" %.0f", (double)st[bmx * 8 + i] / tpc);
+        printf(" per tile)\n");
     }
 #endif
     fflush(stdout);
 }
 
 // histogram geometry: THREADS per workgroup, `split` workgroups per chunk, `chunks` chunks
-template <int THREADS, int NT = 0>
+template <int THREADS, int NT = 0, int SUB = 1>
 void hist_variant(Ctx &c, const char *name, uint32_t chunks, uint32_t split) {
     if (g_filter && !strstr(name, g_filter)) return;
     HistArgs h{};
@@ -171,7 +186,7 @@ void hist_variant(Ctx &c, const char *name, uint32_t chunks, uint32_t split) {
     h.split = split;
     const float ms = time_ms(c, 5, [&] {
         hipMemsetAsync(c.table, 0, (size_t)chunks * 256 * 4, 0);
-        rs_histogram<8, THREADS, kDigitShift, NT><<<chunks * split, THREADS>>>(h);
+        rs_histogram<8, THREADS, kDigitShift, NT, SUB><<<chunks * split, THREADS>>>(h);
     });
     printf("%-34s grid=%-6u %8.3f ms  %7.1f GB/s (read)\n", name, chunks * split, ms, 4.0 * c.n / ms / 1e6);
     fflush(stdout);
@@ -195,6 +210,23 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&c.e0));
     CK(hipEventCreate(&c.e1));
     CK(launch_gen_uniform(c.keys, c.n, 0x5EED, 0));
+    if (getenv("LAB_ZIPF")) {  // Zipf(1.0) over 2^20 ranks, key = fmix32(rank) (== rsort_gen_zipf)
+        const uint64_t ranks = 1u << 20;
+        std::vector<double> cum(ranks);
+        double acc = 0;
+        for (uint64_t r = 0; r < ranks; ++r) cum[r] = (acc += 1.0 / (double)(r + 1));
+        std::vector<uint32_t> cdf(ranks);
+        for (uint64_t r = 0; r < ranks; ++r) {
+            const double t = floor(cum[r] / acc * 4294967296.0);
+            cdf[r] = (uint32_t)(t > 4294967295.0 ? 4294967295.0 : t);
+        }
+        cdf[ranks - 1] = 4294967295u;
+        uint32_t *dcdf;
+        CK(hipMalloc(&dcdf, ranks * 4));
+        CK(hipMemcpy(dcdf, cdf.data(), ranks * 4, hipMemcpyHostToDevice));
+        CK(launch_gen_zipf(c.keys, c.n, 0x5EED, dcdf, ranks, 0));
+        printf("keys: zipf\n");
+    }
     CK(launch_gen_iota(c.vals, c.n, 0, 0));
     CK(hipDeviceSynchronize());
     printf("n=%llu cus=%d\n", (unsigned long long)c.n, c.cus);
@@ -209,19 +241,20 @@ int main(int argc, char **argv) {
     }
 #ifdef LINES_ONLY
     // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
-    hist_variant<1024>(c, "hist 1024 x4", 256, 4);
-    hist_variant<1024, 1>(c, "hist 1024 x4 nt", 256, 4);
-    hist_variant<1024>(c, "hist 1024 x8", 256, 8);
-    hist_variant<1024, 1>(c, "hist 1024 x8 nt", 256, 8);
-    hist_variant<512, 1>(c, "hist 512 x8 nt", 256, 8);
-    hist_variant<1024, 1>(c, "hist 1024 x2 nt", 256, 2);
-    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32", 1.0);
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 ntboth", 1.0);
-    lines<8, 1024, 16, 32, false>(c, "k8 1024x16 lines32 again", 1.0);
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 ntboth again", 1.0);
-    c.have_ref = false;
-    lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
-    lines<8, 512, 16, 16, true, true, 0, 3>(c, "k8 pairs 512x16 lines16 ntboth", 1.0);
+    lines<8, 1024, 16, 32, false, true, 4, 3>(c, "k8 1024x16 lines32 nt plain", 1.0);
+    lines<8, 1024, 16, 32, false, true, 24, 3>(c, "k8 1024x16 lines32 nt firstlane", 1.0);
+    lines<8, 1024, 16, 32, false, true, 8, 3>(c, "k8 1024x16 lines32 nt match", 1.0);
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt adaptive", 1.0);
+    {
+        // second pass shape: the first pass's output (clustered by digit 0) as input
+        std::swap(c.keys, c.out);
+        printf("input: pass-1 output\n");
+        c.have_ref = false;
+        lines<8, 1024, 16, 32, false, true, 4, 3>(c, "k8 1024x16 lines32 nt plain (shift 8)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 24, 3>(c, "k8 1024x16 lines32 nt firstlane (shift 8)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 8, 3>(c, "k8 1024x16 lines32 nt match (shift 8)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt adaptive (shift 8)", 1.0, 8);
+    }
     return 0;
 #endif
     hist_variant<256>(c, "hist 256 x8", 256, 8);
