@@ -241,19 +241,20 @@ int main(int argc, char **argv) {
     }
 #ifdef LINES_ONLY
     // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
-    lines<8, 1024, 16, 32, false, true, 4, 3>(c, "k8 1024x16 lines32 nt plain", 1.0);
-    lines<8, 1024, 16, 32, false, true, 24, 3>(c, "k8 1024x16 lines32 nt firstlane", 1.0);
-    lines<8, 1024, 16, 32, false, true, 8, 3>(c, "k8 1024x16 lines32 nt match", 1.0);
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt adaptive", 1.0);
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
+    lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom", 1.0);
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt again", 1.0);
+    lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom again", 1.0);
     {
         // second pass shape: the first pass's output (clustered by digit 0) as input
         std::swap(c.keys, c.out);
         printf("input: pass-1 output\n");
         c.have_ref = false;
-        lines<8, 1024, 16, 32, false, true, 4, 3>(c, "k8 1024x16 lines32 nt plain (shift 8)", 1.0, 8);
-        lines<8, 1024, 16, 32, false, true, 24, 3>(c, "k8 1024x16 lines32 nt firstlane (shift 8)", 1.0, 8);
-        lines<8, 1024, 16, 32, false, true, 8, 3>(c, "k8 1024x16 lines32 nt match (shift 8)", 1.0, 8);
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt adaptive (shift 8)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (shift 8)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom (shift 8)", 1.0, 8);
+        c.have_ref = false;
+        lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16 (shift 8)", 1.0, 8);
+        lines<8, 512, 16, 16, true, true, 32>(c, "k8 pairs 512x16 lines16 nodom (shift 8)", 1.0, 8);
     }
     return 0;
 #endif
