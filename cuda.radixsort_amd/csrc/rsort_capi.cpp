@@ -99,7 +99,10 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
-    if (k <= 4 && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
+    // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
+    // lines: 2^26 keys, k = 4: 0.117 vs 0.144 ms per pass, dev/scatter_lab.hip); k <= 2 keeps
+    // rs_scatter's 8192-key tiles
+    if (k <= 2 && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     return kGeomSmall;
 }
 

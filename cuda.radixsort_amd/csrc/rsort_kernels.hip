@@ -1294,7 +1294,16 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         if (geom == kGeomSmall) return scatter_fn<BITS, PAIRS, kRankSplit, kDigitShift, kGeomSmall>();
         return nullptr;
     }
-    if (geom == kGeomSmall) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
+    if (geom == kGeomSmall) {
+        if constexpr (BITS >= 3 && BITS <= 4 && !PAIRS) {
+            // k = 3, 4 keys: whole 128-B lines from 4096-key tiles (lane-ordered atomics and 16-B
+            // aligned outputs, like kGeomLines)
+            constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
+            if (rank == kRankAtomic && aligned16)
+                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, true, 0, 3>);
+        }
+        return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
+    }
     if constexpr (BITS >= 5 && BITS <= 8) {
         if (geom == kGeomLarge) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLarge>(rank);
         // whole-line stores need lane-ordered atomics and 16-B aligned outputs; else the same

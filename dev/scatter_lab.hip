@@ -241,21 +241,20 @@ int main(int argc, char **argv) {
     }
 #ifdef LINES_ONLY
     // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
-    lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom", 1.0);
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt again", 1.0);
-    lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom again", 1.0);
-    {
-        // second pass shape: the first pass's output (clustered by digit 0) as input
-        std::swap(c.keys, c.out);
-        printf("input: pass-1 output\n");
+    if (getenv("LAB_K4")) {
+        variant<4, 512, 16, false, kRankAtomic, 4>(c, "k4 512x16 atomic w4 (lib)", 1.0);
+        lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt", 1.0);
+        lines<4, 256, 16, 32, false, true, 0, 1>(c, "k4 256x16 lines32 ntload", 1.0);
+        lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt again", 1.0);
         c.have_ref = false;
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (shift 8)", 1.0, 8);
-        lines<8, 1024, 16, 32, false, true, 32, 3>(c, "k8 1024x16 lines32 nt nodom (shift 8)", 1.0, 8);
+        variant<3, 512, 16, false, kRankAtomic, 4>(c, "k3 512x16 atomic w4 (lib)", 1.0);
+        lines<3, 256, 16, 32, false, true, 0, 3>(c, "k3 256x16 lines32 nt", 1.0);
         c.have_ref = false;
-        lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16 (shift 8)", 1.0, 8);
-        lines<8, 512, 16, 16, true, true, 32>(c, "k8 pairs 512x16 lines16 nodom (shift 8)", 1.0, 8);
+        variant<2, 512, 16, false, kRankAtomic, 4>(c, "k2 512x16 atomic w4 (lib)", 1.0);
+        lines<2, 256, 16, 32, false, true, 0, 3>(c, "k2 256x16 lines32 nt", 1.0);
+        return 0;
     }
+    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
     return 0;
 #endif
     hist_variant<256>(c, "hist 256 x8", 256, 8);

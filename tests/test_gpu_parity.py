@@ -97,14 +97,15 @@ def test_distributions(dist):
             assert np.array_equal(gpu_sort(x, k, algo), oracle_sort(x, k)), (dist, k, algo)
 
 
-@pytest.mark.parametrize("k", [8, 6, 5, 4, 3])
+@pytest.mark.parametrize("k", [8, 6, 5, 4, 3, 2])
 def test_large_tile_geometries(k):
-    """n >= 2 * CUs * tile selects the 16384-key (k = 5..8) / 8192-key (k <= 4) tiles; ragged
-    tails and zipf keys, keys and pairs, against the oracle."""
+    """n >= 2 * CUs * tile selects the 16384-key line tiles (k = 5..8), 4096-key line tiles
+    (k = 3, 4) or 8192-key tiles (k <= 2); ragged tails and zipf keys, keys and pairs, against
+    the oracle."""
     n = (1 << 23) + 12345
     keys = zipf_keys(n, seed=k) if k % 2 else uniform_keys(n, seed=k)
     p = rs.plan(n, k, False)
-    assert p.tile_keys in (8192, 16384), p.as_dict()
+    assert p.tile_keys == {8: 16384, 6: 16384, 5: 16384, 4: 4096, 3: 4096, 2: 8192}[k], p.as_dict()
     assert np.array_equal(gpu_sort(keys, k), oracle_sort(keys, k))
     if k >= 5:
         vals = np.arange(n, dtype=np.uint32)
@@ -123,7 +124,7 @@ def test_lane_order_probe():
 @pytest.mark.parametrize("dist", ["uniform", "zipf", "allsame", "fewdigits"])
 @pytest.mark.parametrize("tpc", [0, 1, 3, 7])
 def test_whole_line_scatter(dist, tpc):
-    """k = 5..8 keys at n >= 2 * CUs * 16384 run rs_scatter_lines (whole 64-B lines, per-digit
+    """k = 5..8 keys at n >= 2 * CUs * 16384 run rs_scatter_lines (whole 128-B lines, per-digit
     carries across tiles, masked first/last lines per chunk): chunk geometries, skew, ragged n."""
     n = (1 << 23) + 4099
     if dist == "uniform":
@@ -151,6 +152,26 @@ def test_whole_line_scatter_misaligned_output_falls_back():
         rs.sort_device(dev(x), out, 8)
         torch.cuda.synchronize()
         assert np.array_equal(host(out), oracle_sort(x, 8)), off
+
+
+def test_whole_line_scatter_16b_aligned_output():
+    """A 16-B but not 128-B aligned output keeps the line kernel (its lines then straddle the
+    L2 lines: slower, same result); keys and pairs."""
+    n = (1 << 23) + 333
+    x = zipf_keys(n, seed=9)
+    vals = np.arange(n, dtype=np.uint32)
+    rk, rv = oracle_sort_pairs(x, vals, 8)
+    big = rs.empty_u32(n + 32)
+    bigv = rs.empty_u32(n + 32)
+    for off in (4, 8, 28):
+        out = big[off:off + n]
+        rs.sort_device(dev(x), out, 8)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(out), rk), off
+        vout = bigv[off:off + n]
+        rs.sort_device(dev(x), out, 8, vals_in=dev(vals), vals_out=vout)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(out), rk) and np.array_equal(host(vout), rv), off
 
 
 @pytest.mark.parametrize("tpc", [1, 2, 3, 17])
