@@ -8,15 +8,18 @@
 # Output: gpurun_out/prof_${TAG}/ ; profiles/summarize.py turns it into the committed summaries.
 set -euo pipefail
 TAG="${1:-r01}"
+shift || true
+ARGS="$*"   # extra bench.py arguments, e.g. "--dist zipf --pairs" or "--keys 67108864 --k 4"
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 OUT="$R/gpurun_out/prof_${TAG}"
+rm -rf "$OUT"   # rocprofv3 writes per-process subdirectories: start clean
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -- \
-    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu > "$OUT/bench_trace.log" 2>&1 &&
+    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu $ARGS > "$OUT/bench_trace.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu > "$OUT/bench_fetch.log" 2>&1 &&
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu $ARGS > "$OUT/bench_fetch.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu > "$OUT/bench_write.log" 2>&1
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu $ARGS > "$OUT/bench_write.log" 2>&1
 echo "profiles written to $OUT"

@@ -1,6 +1,7 @@
 """Turn a profiles/run_profiles.sh output directory into the committed summaries.
 
-    python profiles/summarize.py gpurun_out/prof_r01 r01
+    python profiles/summarize.py gpurun_out/prof_r01 r01                      # C3 (default config)
+    python profiles/summarize.py gpurun_out/prof_r01_c4 r01 --dist zipf --pairs --stats-tag r01_c4
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
 profiles/<tag>_pmc.json: per-kernel FETCH_SIZE / WRITE_SIZE per launch and the HBM bytes per
@@ -31,16 +32,18 @@ def _counters(path: Path):
 
 
 def _one(glob_dir: Path, pattern: str) -> Path:
-    hits = sorted(glob_dir.rglob(pattern))
+    """The newest match: rocprofv3 adds a per-process subdirectory, so reruns accumulate."""
+    hits = sorted(glob_dir.rglob(pattern), key=lambda p: p.stat().st_mtime)
     if not hits:
         raise SystemExit(f"no {pattern} under {glob_dir}")
-    return hits[0]
+    return hits[-1]
 
 
-def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
+def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform", pairs: bool = False,
+         stats_tag: str | None = None):
     src = Path(src)
     stats = _one(src / "trace", "*kernel_stats.csv")
-    shutil.copy(stats, HERE / f"{tag}_kernel_stats.csv")
+    shutil.copy(stats, HERE / f"{stats_tag or tag}_kernel_stats.csv")
     fetch = _counters(_one(src / "pmc_fetch", "*counter_collection.csv"))
     write = _counters(_one(src / "pmc_write", "*counter_collection.csv"))
 
@@ -49,7 +52,7 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
         return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
     hist_fetch, _ = per_launch(fetch, "FETCH_SIZE", "rs_histogram")
-    gen_write, _ = per_launch(write, "WRITE_SIZE", "rs_gen_uniform")
+    gen_write, _ = per_launch(write, "WRITE_SIZE", "rs_gen_uniform" if dist == "uniform" else "rs_gen_zipf")
     sc_fetch, nf = per_launch(fetch, "FETCH_SIZE", "rs_scatter")
     sc_write, nw = per_launch(write, "WRITE_SIZE", "rs_scatter")
     kib = 1024.0
@@ -57,23 +60,27 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
     write_ratio = (gen_write * kib) / (4.0 * n) if gen_write else 1.0
     read_bytes = sc_fetch * kib / fetch_ratio
     write_bytes = sc_write * kib / write_ratio
-    algo = 8.0 * n
+    algo = (16.0 if pairs else 8.0) * n
     names = {kn for (kn, c) in list(fetch) + list(write) if "rs_scatter" in kn}
     kernel = "rs_scatter_lines" if any("rs_scatter_lines" in kn for kn in names) else "rs_scatter"
     rows = {}
     for (kn, c), vs in sorted(fetch.items()) + sorted(write.items()):
         rows.setdefault(kn, {})[c + "_KiB_per_launch"] = sum(vs) / len(vs)
         rows[kn]["launches_" + c] = len(vs)
+    path = HERE / f"{tag}_pmc.json"
+    prev = json.loads(path.read_text()) if path.exists() else {}
+    cfg = f"n{n}_k{k}_{dist}_{'pairs' if pairs else 'keys'}_match:{kernel}"
     out = {
-        "source": f"profiles/run_profiles.sh {tag} (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
-                  f"separate passes; bench.py --steps 2 --warmup 1 at n={n}, k={k})",
+        "source": f"profiles/run_profiles.sh {tag} [bench args] (rocprofv3 --pmc FETCH_SIZE, then --pmc "
+                  f"WRITE_SIZE, separate passes; bench.py --steps 2 --warmup 1); one entry per config",
         "calibration": {"fetch_ratio_measured": round(fetch_ratio, 4),
                         "fetch_ratio_note": "rs_histogram reads exactly 4n bytes with 16-B loads; "
                                             "gfx950 FETCH_SIZE reports half (MI355X_MICROARCH.md HBM)",
                         "write_ratio_measured": round(write_ratio, 4),
                         "write_ratio_note": "rs_gen_uniform writes exactly 4n bytes with dword stores"},
         "configs": {
-            f"n{n}_k{k}_uniform_keys_match:{kernel}": {
+            **prev.get("configs", {}),
+            cfg: {
                 "kernel": f"{kernel} (fused local sort + rank + scatter)",
                 "kernel_symbols": sorted(names),
                 "launches": {"fetch_pass": nf, "write_pass": nw},
@@ -82,13 +89,24 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8):
                 "hbm_bytes_per_launch": read_bytes + write_bytes,
                 "algorithmic_bytes_per_launch": algo,
                 "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
+                "calibration": {"fetch_ratio": round(fetch_ratio, 4), "write_ratio": round(write_ratio, 4)},
             }
         },
-        "per_kernel_raw": rows,
+        "per_kernel_raw": {**prev.get("per_kernel_raw", {}), cfg: rows},
     }
-    (HERE / f"{tag}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
-    print(json.dumps(out["configs"], indent=1))
+    path.write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps(out["configs"][cfg], indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("tag")
+    ap.add_argument("--keys", type=int, default=1 << 30)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--dist", default="uniform")
+    ap.add_argument("--pairs", action="store_true")
+    ap.add_argument("--stats-tag", default=None)
+    a = ap.parse_args()
+    main(a.src, a.tag, a.keys, a.k, a.dist, a.pairs, a.stats_tag)
