@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--vendor", action="store_true", help="also time rocPRIM's radix sort")
+    ap.add_argument("--no-group-chunks", action="store_true",
+                    help="every pass counts its own histogram (no digit-group chunks)")
     return ap.parse_args()
 
 
@@ -120,6 +122,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
+    rs.set_group_chunks(not a.no_group_chunks)
 
     n = a.n
     seed = 0x5EED + rank * n  # one global splitmix stream, block-distributed by index
@@ -166,6 +169,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     barrier()
+    groups = rs.group_flags(p, ws) if world == 1 else None
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
@@ -219,6 +223,8 @@ def main():
                        "keys_per_gpu": n, "k_bits": a.k, "passes": p.passes, "dist": a.dist,
                        "pairs": bool(a.pairs), "rank_algo": a.rank, "tile_keys": p.tile_keys,
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
+                       "group_chunk_passes": ([2 * i + 1 for i, f in enumerate(groups) if f]
+                                              if groups is not None else None),
                        "parallelism": "single GPU" if world == 1 else f"range-partition x{world} (RCCL all-to-all)"},
             "roofline": {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

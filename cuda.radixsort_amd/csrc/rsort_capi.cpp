@@ -25,6 +25,7 @@ namespace {
 
 constexpr int kVersion = 100;  // 0.1.0
 std::atomic<int> g_rank_algo{RSORT_RANK_MATCH};
+std::atomic<int> g_group_chunks{1};
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -106,6 +107,13 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     return kGeomSmall;
 }
 
+// Digit-group chunks (rs_histogram_joint, rsort_kernels.hip): k = 8 plans with exactly 2^8
+// chunks of line tiles. Every second pass then reads no keys for its histogram.
+bool joint_plan(const rsort_plan &p) {
+    return p.k_bits == kJointBits && p.num_chunks == (int64_t)kJointBins && p.passes >= 2 &&
+           (geom_from_shape(p.threads, p.tile_keys, p.pairs) == (p.pairs ? kGeomLinesPairs : kGeomLines));
+}
+
 int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int partition = 0) {
     if (!p) return RSORT_ERR_ARG;
     if (k < kMinBits || k > kMaxBits) return RSORT_ERR_BITS;
@@ -141,12 +149,16 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     ws += align256((size_t)p->table_entries * 4);            // chunk x digit table
     ws += align256((size_t)p->scan_blocks * 4);              // scan block sums
     ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
+    if (joint_plan(*p)) {
+        ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
+        ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
+    }
     p->workspace_bytes = ws;
     return RSORT_OK;
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -163,13 +175,46 @@ Carve carve(const rsort_plan &p, void *ws) {
     c.bsums = (uint32_t *)q;
     q += align256((size_t)p.scan_blocks * 4);
     c.starts = (uint32_t *)q;
+    q += align256((size_t)(p.bins + 1) * 4);
+    if (joint_plan(p)) {
+        c.joint = (uint32_t *)q;
+        q += align256((size_t)kJointBins * kJointBins * 4);
+        c.bounds = (uint32_t *)q;
+    }
     return c;
 }
 
 // ------------------------------------------------------------------------------ pass pieces
-int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
-                 int dmode, const uint32_t *split, int nsplit, hipStream_t s) {
+// Joint pass (pass p of a joint_plan counting for pass p + 1): one workgroup per chunk counts
+// this pass's table and the joint counts; then the group bounds of pass p + 1. enable: nullptr,
+// or the previous joint pass's flag (its groups were unbalanced: count no joint either).
+int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
+                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, hipStream_t s) {
     HistArgs a{};
+    a.keys = keys;
+    a.table = table;
+    a.n = (uint64_t)p.n;
+    a.chunk_keys = (uint64_t)p.chunk_keys;
+    a.num_chunks = (uint32_t)p.num_chunks;
+    a.shift = (uint32_t)shift;
+    a.vec = (((uintptr_t)keys & 15u) == 0) ? 1u : 0u;
+    a.split = 1;
+    a.joint = joint;
+    a.joint_enable = enable;
+    PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
+    if (hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess) return RSORT_ERR_HIP;
+    if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
+    // a group may take one tile more than a fixed chunk
+    return hip_status(launch_joint_bounds(joint, enable, bounds, (uint64_t)p.n,
+                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, s));
+}
+
+int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
+                 int dmode, const uint32_t *split, int nsplit, hipStream_t s,
+                 const uint32_t *bounds = nullptr, const uint32_t *copy_src = nullptr) {
+    HistArgs a{};
+    a.bounds = bounds;
+    a.copy_src = copy_src;
     a.keys = keys;
     a.table = table;
     a.n = (uint64_t)p.n;
@@ -203,8 +248,9 @@ int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s
 
 int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
-               const uint32_t *split, int nsplit, hipStream_t s) {
+               const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr) {
     ScatterArgs a{};
+    a.bounds = bounds;
     a.kin = kin;
     a.vin = vin;
     a.kout = kout;
@@ -221,6 +267,8 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
+    if (bounds && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
+        return RSORT_ERR_ARG;  // group chunks: rs_scatter_lines only
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
     return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, local_only ? 0 : aligned16, a, s));
 }
@@ -262,14 +310,33 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         sk = c.tmp_k;
         sv = c.tmp_v;
     }
+    // digit-group chunks on every second pass (joint_plan): needs rs_scatter_lines for both
+    // outputs (lane-ordered ranks, 16-B aligned ping-pong buffers)
+    const bool joint = joint_plan(p) && g_group_chunks.load() != 0 &&
+                       internal_rank(g_rank_algo.load()) == kRankAtomic &&
+                       ((((uintptr_t)kout) | (uintptr_t)c.tmp_k |
+                         (p.pairs ? ((uintptr_t)vout | (uintptr_t)c.tmp_v) : 0u)) & 15u) == 0;
+    if (joint_plan(p) && !joint &&
+        hipMemsetAsync(c.bounds, 0, (size_t)2 * kBoundsWords * 4, s) != hipSuccess)  // rsort_group_flags: none
+        return RSORT_ERR_HIP;
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
         const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
         uint32_t *dk = to_out ? kout : c.tmp_k;
         uint32_t *dv = to_out ? vout : c.tmp_v;
-        if ((st = do_histogram(p, sk, shift, c.table, kDigitShift, nullptr, 0, s))) return st;
+        // even pass i counts the joint counts for pass i + 1; odd pass i may use them
+        const bool count_joint = joint && (i % 2 == 0) && i + 1 < P;
+        const uint32_t *bounds = (joint && (i % 2 == 1)) ? c.bounds + (i / 2) * kBoundsWords : nullptr;
+        if (count_joint) {
+            const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
+            if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
+                                         c.bounds + (i / 2) * kBoundsWords, s)))
+                return st;
+        } else if ((st = do_histogram(p, sk, shift, c.table, kDigitShift, nullptr, 0, s, bounds, c.joint))) {
+            return st;
+        }
         if ((st = do_scan(p, c.table, c.bsums, s))) return st;
-        if ((st = do_scatter(p, sk, sv, dk, dv, shift, c.table, 0, kDigitShift, nullptr, 0, s)))
+        if ((st = do_scatter(p, sk, sv, dk, dv, shift, c.table, 0, kDigitShift, nullptr, 0, s, bounds)))
             return st;
         sk = dk;
         sv = dv;
@@ -483,6 +550,32 @@ int rsort_set_rank_algo(int algo) {
 }
 
 int rsort_get_rank_algo(void) { return g_rank_algo.load(); }
+
+int rsort_set_group_chunks(int enable) {
+    g_group_chunks.store(enable ? 1 : 0);
+    return RSORT_OK;
+}
+
+int rsort_get_group_chunks(void) { return g_group_chunks.load(); }
+
+int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream) {
+    if (!plan || !flags || !d_workspace) return RSORT_ERR_ARG;
+    int st = check_plan(plan);
+    if (st) return st;
+    flags[0] = flags[1] = 0;
+    if (!joint_plan(*plan) || plan->n == 0) return RSORT_OK;
+    const Carve c = carve(*plan, const_cast<void *>(d_workspace));
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h[2] = {0, 0};
+    for (int i = 0; i < 2; ++i)
+        if (2 * i + 1 < plan->passes &&
+            hipMemcpyAsync(&h[i], c.bounds + i * kBoundsWords, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    flags[0] = h[0] ? 1 : 0;
+    flags[1] = h[1] ? 1 : 0;
+    return RSORT_OK;
+}
 
 int rsort_lane_order_probe(void) {
     int count = 0;

@@ -64,6 +64,15 @@ struct HistArgs {
     uint32_t split;         // workgroups per chunk (> 1: partial counts added into a zeroed table)
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
+    // Digit-group chunks (kJointBits plans, see rs_histogram_joint). bounds != nullptr and
+    // bounds[0] != 0: this pass's table is copy_src (the previous pass's joint counts), copied
+    // instead of counted.
+    const uint32_t *bounds;
+    const uint32_t *copy_src;
+    // rs_histogram_joint only: the joint counts [next digit][digit] are added into `joint`
+    // (zeroed); joint_enable == nullptr or *joint_enable != 0 turns the joint count on.
+    uint32_t *joint;
+    const uint32_t *joint_enable;
 };
 
 struct ScatterArgs {
@@ -80,6 +89,10 @@ struct ScatterArgs {
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
     unsigned long long *stamps;  // diagnostic builds (RSORT_STAMPS) only: per-phase cycles
+    // rs_scatter_lines only: bounds != nullptr and bounds[0] != 0 -> chunk c is the key range
+    // [bounds[1 + c], bounds[2 + c]) (a digit group of the previous pass) instead of
+    // [c * chunk_keys, (c + 1) * chunk_keys)
+    const uint32_t *bounds;
 };
 
 struct ScanArgs {
@@ -91,6 +104,19 @@ struct ScanArgs {
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.
 hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t s);
+// Digit-group chunks: k = 8 and exactly 2^8 chunks. Pass p counts, besides its own per-chunk
+// table, the joint counts of (digit p, digit p + 1) over all keys; pass p + 1's chunks are then
+// the digit-p groups of pass p's output, whose per-chunk counts ARE those joint counts, so pass
+// p + 1 reads no keys for its histogram.
+constexpr int kJointBits = 8;
+constexpr uint32_t kJointBins = 1u << kJointBits;
+constexpr uint32_t kBoundsWords = kJointBins + 2;  // {flag, group starts[0..R]}
+hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
+// From the joint counts [next digit][group]: group starts into bounds[1..R+1] and bounds[0] = 1
+// when every group fits in max_keys keys and the counts add up to n (else 0: the next pass
+// counts its own histogram over fixed chunks). enable: as HistArgs::joint_enable.
+hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
+                               uint64_t n, uint64_t max_keys, hipStream_t s);
 // rank_algo: internal RankAlgo. aligned16: kout/vout 16-B aligned (kGeomLines line stores;
 // otherwise the same plan runs rs_scatter with the same tiles).
 hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom, int aligned16,

@@ -209,18 +209,113 @@ struct Digit {
 // SUB: each per-wave copy is split into SUB interleaved sub-counters (lane % SUB picks one), so
 // lanes of one instruction that share a digit -- the common digits of skewed keys -- hit SUB
 // different addresses instead of serialising on one.
-template <int BITS, int THREADS, int DMODE, int NT = 0, int SUB = 1>
+//
+// Digit-group chunks (k = 8, 2^8 chunks; rsort_capi.cpp sort_planned). After pass p the keys are
+// ordered by digit p, so pass p + 1 may take digit p's groups as its chunks: group g's counts of
+// digit p + 1 are the joint counts J[g][.] of (digit p, digit p + 1), which pass p counts here
+// (JOINT) while it reads the keys anyway. Pass p + 1's histogram launch then only copies them
+// (a.bounds[0] set by rs_joint_bounds when the groups are balanced enough to be chunks).
+// Joint counts live in LDS as 2^16 16-bit counters, two per word, in rows of 128 + 1 words
+// (the pad makes the column sweep of the final add bank-conflict free); a counter that reaches
+// 2^15 moves 2^15 to its row's spill word and to the global count (the returning add tells).
+template <int THREADS>
+__device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j, uint32_t c,
+                                                uint32_t sub, uint32_t S) {
+    constexpr uint32_t R = kJointBins;
+    constexpr uint32_t RS = R / 2 + 1;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t *s_sp = s_j + R * RS;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
+    __syncthreads();
+    const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
+    auto add = [&](uint32_t x) {
+        const uint32_t d = (x >> s0) & (R - 1u), e = (x >> s1) & (R - 1u);
+        const uint32_t wi = d * RS + (e >> 1), sh = (e & 1u) << 4;
+        const uint32_t old = atomicAdd(&s_j[wi], 1u << sh);
+        if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+            atomicSub(&s_j[wi], 0x8000u << sh);
+            atomicAdd(&s_sp[d], 0x8000u);
+            atomicAdd(&a.joint[e * R + d], 0x8000u);
+        }
+    };
+    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
+    const uint64_t beg = min(cbeg + sub * part, cend);
+    const uint64_t end = min(beg + part, cend);
+    uint64_t tail = beg;
+    if (a.vec) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
+        const uint32_t nvec = (uint32_t)((end - beg) / 4);
+        constexpr int U = 4;
+        for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
+            u32x4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = v0 + u * THREADS;
+                q[u] = v < nvec ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (v0 + u * THREADS < nvec) {
+                    add(q[u].x);
+                    add(q[u].y);
+                    add(q[u].z);
+                    add(q[u].w);
+                }
+            }
+        }
+        tail = beg + (uint64_t)nvec * 4;
+    }
+    for (uint64_t i = tail + t; i < end; i += THREADS) add(a.keys[i]);
+    __syncthreads();
+    // this chunk's digit counts: row sums plus the row's spill
+    for (uint32_t d = t; d < R; d += THREADS) {
+        uint32_t s = s_sp[d];
+        for (uint32_t j = 0; j < R / 2; ++j) {
+            const uint32_t x = s_j[d * RS + j];
+            s += (x & 0xFFFFu) + (x >> 16);
+        }
+        if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = s;
+        else if (s) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], s);
+    }
+    // joint counts -> global [e][d] (consecutive lanes: consecutive d, one contiguous 256-B add)
+    for (uint32_t item = t; item < R * R; item += THREADS) {
+        const uint32_t e = item / R, d = item % R;
+        const uint32_t v = (s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu;
+        if (v) atomicAdd(&a.joint[item], v);
+    }
+}
+
+template <int BITS, int THREADS, int DMODE, int NT = 0, int SUB = 1, bool JOINT = false>
 __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int HW = (R * W <= 4096) ? W : 1;  // per-wave private copies when they fit (<= 16 KB)
     constexpr int SB = HW > 1 ? SUB : 1;
-    __shared__ uint32_t s_h[HW * R * SB];
+    constexpr uint32_t PLAIN = HW * R * SB;
+    constexpr uint32_t JW = kJointBins * (kJointBins / 2 + 1) + kJointBins;
+    static_assert(!JOINT || (BITS == kJointBits && DMODE == kDigitShift), "joint counts: k = 8 digits");
+    __shared__ uint32_t s_h[(JOINT && JW > PLAIN) ? JW : PLAIN];
 
     const uint32_t t = threadIdx.x;
     const uint32_t S = a.split;
     const uint32_t c = blockIdx.x / S;
     const uint32_t sub = blockIdx.x % S;
+    if (a.bounds != nullptr && a.bounds[0] != 0u) {
+        // digit-group chunks: this pass's table is the previous pass's joint counts
+        const uint64_t m = (uint64_t)R * a.num_chunks;
+        for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < m; i += (uint64_t)gridDim.x * THREADS)
+            a.table[i] = a.copy_src[i];
+        return;
+    }
+    if constexpr (JOINT) {
+        if (a.joint_enable == nullptr || *a.joint_enable != 0u) {
+            hist_joint_body<THREADS>(a, s_h, c, sub, S);
+            return;
+        }
+    }
     for (uint32_t i = t; i < HW * R * SB; i += THREADS) s_h[i] = 0;
     __syncthreads();
 
@@ -327,6 +422,43 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
     for (int i = 0; i < kScanPerThread; ++i) {
         if (base + i < a.m) a.table[base + i] = run;
         run += v[i];
+    }
+}
+
+// ------------------------------------------------------------------------------ group bounds
+// One workgroup: group totals (column sums of the joint counts [next digit][group]), their
+// exclusive scan = the groups' first key positions in the previous pass's output, and the flag
+// that lets the next pass use them as chunks.
+__global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, const uint32_t *enable,
+                                                        uint32_t *bounds, uint64_t n, uint64_t max_keys) {
+    constexpr uint32_t R = kJointBins;
+    constexpr uint32_t Q = 1024 / R;
+    __shared__ uint32_t s_part[Q][R];
+    __shared__ uint32_t s_ws[1024 / kWave];
+    __shared__ uint32_t s_max;
+    const uint32_t t = threadIdx.x;
+    if (enable != nullptr && *enable == 0u) {
+        if (t == 0) bounds[0] = 0u;
+        return;
+    }
+    const uint32_t g = t % R, q = t / R;
+    uint32_t s = 0;
+    for (uint32_t e = q * (R / Q); e < (q + 1) * (R / Q); ++e) s += joint[e * R + g];
+    s_part[q][g] = s;
+    if (t == 0) s_max = 0u;
+    __syncthreads();
+    uint32_t tot = 0;
+    if (t < R) {
+#pragma unroll
+        for (uint32_t i = 0; i < Q; ++i) tot += s_part[i][t];
+        atomicMax(&s_max, tot);
+    }
+    uint32_t total = 0;
+    const uint32_t start = block_excl_scan<1024>(tot, s_ws, total);
+    if (t < R) bounds[1 + t] = start;
+    if (t == 0) {
+        bounds[1 + R] = total;
+        bounds[0] = ((uint64_t)total == n && (uint64_t)s_max <= max_keys) ? 1u : 0u;
     }
 }
 
@@ -880,8 +1012,18 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     const uint32_t lane = lane_id();
     const uint32_t c = blockIdx.x;
     const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
-    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
-    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    uint32_t head = 0;  // leading keys of the first tile that belong to the previous chunk
+    if (a.bounds != nullptr && a.bounds[0] != 0u) {
+        // digit-group chunk (rs_histogram_joint): any start, so the tiles start at the 256-B
+        // boundary below it (every wave load stays two whole 128-B lines), the first tile skips
+        // its `head` keys, and every chunk may end in a partial tile
+        const uint64_t b = a.bounds[1 + c];
+        cend = a.bounds[2 + c];
+        cbeg = b < cend ? (b & ~(uint64_t)(kWave - 1)) : cend;
+        head = (uint32_t)(b < cend ? b - cbeg : 0);
+    }
 
     // digit group of this thread: digit d = t / TPD; the leader (sub == 0) keeps the state
     const uint32_t d_own = t / TPD;
@@ -964,10 +1106,13 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     RS_STAMP_DECL
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        const bool full = valid == T;
+        const bool full = valid == T && head == 0;
         const uint64_t nb = tb + T;
         uint32_t plim = valid > base ? valid - base : 0u;  // slot j is real iff j * 64 < plim
         asm volatile("" : "+v"(plim));
+        // ... and, in slot 0, iff this lane's tile position is not before the chunk (head)
+        const bool h0 = base >= head;
+        head = 0;
         RS_STAMP_WAIT_LOADS();
         RS_STAMP(0);
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
@@ -996,7 +1141,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = dig(key[j]);
                 uint32_t r = 0;
-                if ((uint32_t)(j * kWave) < plim) r = atomicAdd(&s_cnt[w * R + d], 1u);
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
                 if constexpr (RF) rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         }
@@ -1138,7 +1283,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                     ll[u] = bl >> 16;
                 } else {
                     // padding slots (the grid's last tile only) count into a scratch counter
-                    const uint32_t ci = (full || (uint32_t)(j * kWave) < plim) ? w * R + dd[u] : W * R;
+                    const uint32_t ci = (full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0))) ? w * R + dd[u] : W * R;
                     pp[u] = atomicAdd(&s_cnt[ci], 1u);
                     ll[u] = s_lim[dd[u]];
                 }
@@ -1148,7 +1293,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             for (int u = 0; u < SB; ++u) {
                 const int j = j0 + u;
                 uint32_t idx = pp[u] < ll[u] ? pp[u] : CAP + dd[u] * G + (pp[u] - ll[u]);
-                if (!(full || (uint32_t)(j * kWave) < plim)) idx = CAP + R * G;  // scratch slot
+                if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + R * G;  // scratch slot
                 s_stage[idx] = key[j];
                 if constexpr (PAIRS) s_vstage[idx] = val[j];
             }
@@ -1456,6 +1601,19 @@ int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom) {
 }
 
 #endif  // RSORT_LAB_LITE
+
+hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
+    // one 1024-thread workgroup per chunk (the joint table fills the LDS: one per CU)
+    if (a.num_chunks != kJointBins || a.split != 1 || !a.joint) return hipErrorInvalidValue;
+    rs_histogram<kJointBits, 1024, kDigitShift, 1, 8, true><<<a.num_chunks, 1024, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
+                               uint64_t n, uint64_t max_keys, hipStream_t s) {
+    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, n, max_keys);
+    return hipGetLastError();
+}
 
 hipError_t launch_scan(const ScanArgs &a, hipStream_t s) {
     rs_scan_reduce<<<a.nblocks, kScanThreads, 0, s>>>(a);

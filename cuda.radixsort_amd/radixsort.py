@@ -102,6 +102,9 @@ SIGNATURES = {
     "rsort_pass_local_sort": ([_PP, _vp, _vp, _vp, _vp, _int, _vp], _int),
     "rsort_set_rank_algo": ([_int], _int),
     "rsort_get_rank_algo": ([], _int),
+    "rsort_set_group_chunks": ([_int], _int),
+    "rsort_get_group_chunks": ([], _int),
+    "rsort_group_flags": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_lane_order_probe": ([], _int),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
@@ -264,6 +267,14 @@ def sort_device(keys_in, keys_out, k_bits=8, vals_in=None, vals_out=None, ws=Non
     return keys_out
 
 
+def group_flags(p: Plan, ws, stream=None) -> list[int]:
+    """Which odd passes (1, 3) of the last sort with plan `p` and workspace `ws` ran on digit-group
+    chunks (rsort_group_flags; synchronises the stream)."""
+    flags = (ctypes.c_int * 2)()
+    _check(_lib().rsort_group_flags(ctypes.byref(p), _ptr(ws), flags, _stream(stream)), "rsort_group_flags")
+    return [int(flags[0]), int(flags[1])]
+
+
 def pass_histogram(p: Plan, keys, shift, table, stream=None):
     _check(_lib().rsort_pass_histogram(ctypes.byref(p), _ptr(keys), int(shift), _ptr(table), _stream(stream)),
            "rsort_pass_histogram")
@@ -290,6 +301,15 @@ def set_rank_algo(algo: int):
 
 def get_rank_algo() -> int:
     return int(_lib().rsort_get_rank_algo())
+
+
+def set_group_chunks(enable: bool):
+    """Digit-group chunks on every second k = 8 pass (rsort_set_group_chunks; default on)."""
+    _check(_lib().rsort_set_group_chunks(1 if enable else 0), "rsort_set_group_chunks")
+
+
+def get_group_chunks() -> bool:
+    return bool(_lib().rsort_get_group_chunks())
 
 
 def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
@@ -380,6 +400,16 @@ def rank_algo(algo: int):
         yield
     finally:
         set_rank_algo(old)
+
+
+@contextmanager
+def group_chunks(enable: bool):
+    old = get_group_chunks()
+    set_group_chunks(enable)
+    try:
+        yield
+    finally:
+        set_group_chunks(old)
 
 
 class Profile:

@@ -166,6 +166,17 @@ RSORT_API int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_ke
 /* ---------------------------------------------------------------- options / profiling */
 RSORT_API int rsort_set_rank_algo(int algo); /* rsort_rank_algo, process-wide */
 RSORT_API int rsort_get_rank_algo(void);
+/* Digit-group chunks (default on): for k = 8 plans with 256 chunks, every second pass takes
+ * the previous pass's digit groups as its chunks and reads no keys for its histogram (the
+ * pass before counts (digit, next digit) pairs while it reads them). Off: every pass counts
+ * its own histogram. Same output either way; process-wide. */
+RSORT_API int rsort_set_group_chunks(int enable);
+RSORT_API int rsort_get_group_chunks(void);
+/* After a sort with `plan` and `d_workspace` has completed on `stream`: flags[i] = 1 if odd pass
+ * 2i+1 ran on digit-group chunks, else 0 (i < 2; both 0 for plans without group chunks).
+ * Synchronises the stream. */
+RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
+                                void *stream);
 /* 1 if the current device's LDS returns same-address atomic adds in lane order (the default
  * ranking relies on it and falls back to ballots otherwise), 0 if not, < 0 on error. The
  * probe runs once per device (a few microseconds) and is cached. */

@@ -1,0 +1,130 @@
+"""GPU parity of digit-group chunks (k = 8 plans with 256 chunks; rs_histogram_joint and
+rsort_capi.cpp sort_planned): passes 1 and 3 take the previous pass's digit groups as chunks and
+copy their histogram from the joint (digit, next digit) counts the pass before counted.
+Bit-exact against the oracle (Baseline1.cu:15-64 restated) with the path on and off, and the
+flags say which passes actually ran on groups. Runs on the MI355X box (-m gpu)."""
+import numpy as np
+import pytest
+
+from _rs import rs
+from _util import oracle_sort, oracle_sort_pairs, uniform_keys, zipf_keys
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+LINE_TILE = 16384      # kGeomLines tile (keys)
+PAIRS_TILE = 8192      # kGeomLinesPairs tile
+
+
+def group_plan(n, pairs=False):
+    """Plan with exactly 256 chunks (tiles_per_chunk forced), the shape group chunks need (line
+    tiles need n >= 512 tiles, so ragged sizes sit just under 768 or 1024 tiles)."""
+    tile = PAIRS_TILE if pairs else LINE_TILE
+    tiles = (n + tile - 1) // tile
+    assert tiles % 256 == 0
+    p = rs.plan(n, 8, pairs, tiles // 256)
+    assert p.num_chunks == 256 and p.tile_keys == tile, p.as_dict()
+    return p
+
+
+def run(x, p, vals=None, groups=True):
+    with rs.group_chunks(groups):
+        d_in = rs.from_numpy_u32(x)
+        d_out = rs.empty_u32(x.size)
+        ws = rs.workspace(p.workspace_bytes)
+        if vals is None:
+            rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
+            flags = rs.group_flags(p, ws)
+            assert np.array_equal(rs.to_numpy_u32(d_in), x), "input buffer was modified"
+            return rs.to_numpy_u32(d_out), flags
+        v_in = rs.from_numpy_u32(vals)
+        v_out = rs.empty_u32(x.size)
+        rs.sort_device(d_in, d_out, 8, vals_in=v_in, vals_out=v_out, ws=ws, plan_=p)
+        flags = rs.group_flags(p, ws)
+        return (rs.to_numpy_u32(d_out), rs.to_numpy_u32(v_out)), flags
+
+
+@pytest.mark.parametrize("n", [512 * LINE_TILE, 768 * LINE_TILE - 5, 767 * LINE_TILE + 1, 1024 * LINE_TILE - 77])
+def test_uniform_keys_on_groups(n):
+    x = uniform_keys(n, seed=n)
+    want = oracle_sort(x, 8)
+    y, flags = run(x, group_plan(n))
+    assert flags == [1, 1]
+    assert np.array_equal(y, want)
+    y0, flags0 = run(x, group_plan(n), groups=False)
+    assert flags0 == [0, 0]
+    assert np.array_equal(y0, want)
+
+
+def test_zipf_keys_fall_back():
+    """Zipf digit groups are far from balanced: passes 1 and 3 count their own histograms."""
+    n = 768 * LINE_TILE - 3
+    x = zipf_keys(n, seed=7)
+    y, flags = run(x, group_plan(n))
+    assert flags == [0, 0]
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
+def test_joint_counter_spill():
+    """Chunk c holds only digit pair (c, 0) (32768 or 65536 equal pairs per workgroup): the 16-bit
+    joint counters pass 2^15 and spill, and the groups are exactly the chunks (balanced)."""
+    for tiles in (512, 1024):
+        n = tiles * LINE_TILE
+        rng = np.random.default_rng(tiles)
+        chunk = n // 256
+        c = (np.arange(n, dtype=np.uint64) // chunk).astype(np.uint32)
+        hi = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+        x = (c | (hi << 16)).astype(np.uint32)
+        y, flags = run(x, group_plan(n))
+        assert flags[0] == 1
+        assert np.array_equal(y, oracle_sort(x, 8))
+
+
+def test_empty_groups():
+    """64 of the 256 digit-0 values never occur; the other groups still fit one tile over a chunk."""
+    n = 512 * LINE_TILE
+    rng = np.random.default_rng(5)
+    x = uniform_keys(n, seed=5)
+    d0 = rng.integers(0, 192, n, dtype=np.uint32)
+    d0 = d0 + d0 // 3  # skip every 4th value
+    x = ((x & np.uint32(0xFFFFFF00)) | d0).astype(np.uint32)
+    y, flags = run(x, group_plan(n))
+    assert flags[0] == 1
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
+def test_pass1_balanced_pass3_not():
+    """Uniform low 16 bits, constant digit 2: pass 1 runs on groups, pass 3 falls back."""
+    n = 768 * LINE_TILE - 1
+    x = (uniform_keys(n, seed=9) & np.uint32(0xFF00FFFF)) | np.uint32(0x00AB0000)
+    y, flags = run(x, group_plan(n))
+    assert flags == [1, 0]
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+def test_pairs_on_groups(dist):
+    n = 768 * PAIRS_TILE - 9
+    x = uniform_keys(n, seed=3) if dist == "uniform" else zipf_keys(n, seed=3)
+    v = np.arange(n, dtype=np.uint32)
+    (ko, vo), flags = run(x, group_plan(n, pairs=True), vals=v)
+    assert flags == ([1, 1] if dist == "uniform" else [0, 0])
+    wk, wv = oracle_sort_pairs(x, v, 8)
+    assert np.array_equal(ko, wk) and np.array_equal(vo, wv)
+
+
+def test_default_plan_2p27():
+    """The default plan at 2^27 keys (256 chunks on a 256-CU MI355X) takes the group path."""
+    n = 1 << 27
+    p = rs.plan(n, 8)
+    if p.num_chunks != 256:
+        pytest.skip(f"{p.num_chunks} chunks on this device")
+    d_in = rs.empty_u32(n)
+    rs.gen_uniform(d_in, 0x5EED)
+    d_out = rs.empty_u32(n)
+    ws = rs.workspace(p.workspace_bytes)
+    rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
+    assert rs.group_flags(p, ws) == [1, 1]
+    ref, _ = torch.sort(d_in.to(torch.int64) & 0xFFFFFFFF)
+    got = d_out.to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(got, ref)
