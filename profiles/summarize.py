@@ -51,7 +51,11 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
         vals = [v for (kn, c), vs in agg.items() if c == counter and needle in kn for v in vs]
         return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
-    hist_fetch, _ = per_launch(fetch, "FETCH_SIZE", "rs_histogram")
+    # calibrate on the key-reading histogram launches only (digit-group passes' rs_histogram
+    # launches copy a 256-KiB table instead): those above a quarter of the expected 4n/2 bytes
+    hvals = [v for (kn, c), vs in fetch.items() if c == "FETCH_SIZE" and "rs_histogram" in kn
+             for v in vs if v * 1024.0 > 0.25 * 2.0 * n]
+    hist_fetch = sum(hvals) / len(hvals) if hvals else None
     gen_write, _ = per_launch(write, "WRITE_SIZE", "rs_gen_uniform" if dist == "uniform" else "rs_gen_zipf")
     sc_fetch, nf = per_launch(fetch, "FETCH_SIZE", "rs_scatter")
     sc_write, nw = per_launch(write, "WRITE_SIZE", "rs_scatter")
