@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--vendor", action="store_true", help="also time rocPRIM's radix sort")
+    ap.add_argument("--primitives", action="store_true",
+                    help="time the pass primitives in isolation instead (SURVEY 8f row 3) and exit")
     ap.add_argument("--no-group-chunks", action="store_true",
                     help="every pass counts its own histogram (no digit-group chunks)")
     return ap.parse_args()
@@ -100,6 +102,55 @@ def cpu_baseline(n, k, reps, dist):
             "ms_per_sort": round(med * 1e3, 2)}
 
 
+def primitives(a, dev):
+    """SURVEY 8f row 3 -- the reference's primitive demos (Histogram.cu:17-33,
+    PrefixSum-WorkEfficient.cu:81-216, MatrixTranspose.cu:90-243) as this library's pass
+    primitives, each timed alone on n resident keys with HIP events (median of `steps`): the
+    chunk histogram (its store IS the transpose), the table scan, the block-local sort, the
+    fused rank + scatter, and a plain device copy as the HBM ceiling they are read against."""
+    n, k = a.n, a.k
+    keys = rs.empty_u32(n, dev)
+    rs.gen_uniform(keys, 0x5EED)
+    out = rs.empty_u32(n, dev)
+    p = rs.plan(n, k, False, a.tiles_per_chunk)
+    table = torch.empty(p.table_entries, dtype=torch.int32, device=dev)
+    bsums = torch.empty(max(1, p.scan_blocks), dtype=torch.int32, device=dev)
+
+    def timed(fn):
+        for _ in range(max(1, a.warmup)):
+            fn()
+        ts = []
+        for _ in range(a.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return float(np.median(ts))
+
+    rows = {}
+
+    def row(name, ms, nbytes, what):
+        rows[name] = {"ms": round(ms, 4), "bytes": int(nbytes), "GB/s": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                      "frac_of_peak": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "what": what}
+
+    row("copy", timed(lambda: out.copy_(keys)), 8 * n, "torch device copy (read n + write n)")
+    row("histogram", timed(lambda: rs.pass_histogram(p, keys, 0, table)), 4 * n,
+        "rs_histogram: per-chunk digit counts, stored column-major (histogram + transpose)")
+    rs.pass_histogram(p, keys, 0, table)
+    row("scan", timed(lambda: rs.pass_scan(p, table, bsums)), 8 * p.table_entries,
+        "rs_scan_reduce + rs_scan_down over the table (re-scans its own output: timing only)")
+    rs.pass_histogram(p, keys, 0, table)
+    rs.pass_scan(p, table, bsums)
+    row("scatter", timed(lambda: rs.pass_scatter(p, keys, out, 0, table)), 8 * n,
+        f"{rs.scatter_kernel_name(p)}: block-local rank + global scatter")
+    row("local_sort", timed(lambda: rs.pass_local_sort(p, keys, out, 0)), 8 * n,
+        "block-local stable sort of every tile (sortLocallyDataBlocks' result)")
+    print(json.dumps({"primitives": rows, "keys": n, "k_bits": k, "tile_keys": p.tile_keys,
+                      "num_chunks": p.num_chunks, "steps": a.steps, "peak_GBs": HBM_PEAK_GBS}), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +174,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
     rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
     rs.set_group_chunks(not a.no_group_chunks)
+    if a.primitives:
+        if world == 1:
+            primitives(a, dev)
+        return
 
     n = a.n
     seed = 0x5EED + rank * n  # one global splitmix stream, block-distributed by index

@@ -128,3 +128,29 @@ def test_default_plan_2p27():
     ref, _ = torch.sort(d_in.to(torch.int64) & 0xFFFFFFFF)
     got = d_out.to(torch.int64) & 0xFFFFFFFF
     assert torch.equal(got, ref)
+
+
+def test_in_place_on_groups():
+    """in == out (P = 4: pass 0 reads the caller's buffer, the ping-pong ends in it)."""
+    n = 768 * LINE_TILE - 11
+    x = uniform_keys(n, seed=11)
+    p = group_plan(n)
+    d = rs.from_numpy_u32(x)
+    ws = rs.workspace(p.workspace_bytes)
+    rs.sort_device(d, d, 8, ws=ws, plan_=p)
+    assert rs.group_flags(p, ws) == [1, 1]
+    assert np.array_equal(rs.to_numpy_u32(d), oracle_sort(x, 8))
+
+
+def test_unaligned_output_falls_back():
+    """An output buffer that is not 16-B aligned cannot take the whole-line kernel: fixed chunks."""
+    n = 512 * LINE_TILE
+    x = uniform_keys(n, seed=12)
+    p = group_plan(n)
+    d_in = rs.from_numpy_u32(x)
+    big = rs.empty_u32(n + 1)
+    d_out = big[1:]
+    ws = rs.workspace(p.workspace_bytes)
+    rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
+    assert rs.group_flags(p, ws) == [0, 0]
+    assert np.array_equal(rs.to_numpy_u32(d_out), oracle_sort(x, 8))
