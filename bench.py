@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--vendor", action="store_true", help="also time rocPRIM's radix sort")
+    ap.add_argument("--dist-path", action="store_true",
+                    help="run the multi-GPU sort (partition, RCCL all-to-all, local sort) even on one "
+                         "rank: its overhead against the single-GPU sort")
     ap.add_argument("--primitives", action="store_true",
                     help="time the pass primitives in isolation instead (SURVEY 8f row 3) and exit")
     ap.add_argument("--no-group-chunks", action="store_true",
@@ -166,8 +169,14 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_dist = world > 1 or a.dist_path
+    if use_dist:
         import torch.distributed as dist
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
@@ -197,7 +206,7 @@ def main():
     p = rs.plan(n, a.k, a.pairs, a.tiles_per_chunk)
     ws = rs.workspace(p.workspace_bytes, dev)
 
-    if world > 1:
+    if use_dist:
         import multi
         ops = multi.GpuOps(dev)
 
@@ -224,7 +233,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     barrier()
-    groups = rs.group_flags(p, ws) if world == 1 else None
+    groups = rs.group_flags(p, ws) if not use_dist else None
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
@@ -238,7 +247,7 @@ def main():
     scatter_ms = sc["ms"] / max(1, sc["launches"])
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     achieved = bytes_per_key * keys_per_launch / (scatter_ms * 1e-3) / 1e9
-    kernel = rs.scatter_kernel_name(p) if world == 1 else "rs_scatter"
+    kernel = rs.scatter_kernel_name(p) if not use_dist else "rs_scatter"
     cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel}"
     traffic, traffic_src = traffic_for(cfg_key)
 
@@ -280,7 +289,7 @@ def main():
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
                        "group_chunk_passes": ([2 * i + 1 for i, f in enumerate(groups) if f]
                                               if groups is not None else None),
-                       "parallelism": "single GPU" if world == 1 else f"range-partition x{world} (RCCL all-to-all)"},
+                       "parallelism": "single GPU" if not use_dist else f"range-partition x{world} (RCCL all-to-all)"},
             "roofline": {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -292,10 +301,10 @@ def main():
         }
         if vendor:
             line["vendor"] = vendor
-        if world == 1 and not a.no_cpu:
+        if not use_dist and not a.no_cpu:
             line["cpu_baseline"] = cpu_baseline(min(a.cpu_n, n), a.k, a.cpu_reps, a.dist)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         torch.distributed.destroy_process_group()
 
 

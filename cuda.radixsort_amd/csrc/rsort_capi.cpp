@@ -157,6 +157,14 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     return RSORT_OK;
 }
 
+// Digit bits of a partition into num_buckets key ranges: at least 2, so that the whole-line
+// scatter kernel (a digit's threads inside one wave) takes it.
+int partition_bits(int num_buckets) {
+    int bits = 2;
+    while ((1 << bits) < num_buckets) ++bits;
+    return bits;
+}
+
 struct Carve {
     uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds;
 };
@@ -631,8 +639,7 @@ int rsort_profile_end(rsort_phase_times *out) {
 
 size_t rsort_partition_workspace_size(int64_t n, int num_buckets, int pairs) {
     if (num_buckets < 1 || num_buckets > kMaxSplitters + 1) return 0;
-    int bits = 1;
-    while ((1 << bits) < num_buckets) ++bits;
+    const int bits = partition_bits(num_buckets);
     rsort_plan p;
     if (plan_fill(n, bits, pairs, 0, &p, /*partition=*/1) != RSORT_OK) return 0;
     return p.workspace_bytes;
@@ -646,8 +653,7 @@ int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
     if (num_buckets > 1 && !splitters) return RSORT_ERR_ARG;
     for (int i = 1; i + 1 < num_buckets; ++i)
         if (splitters[i] < splitters[i - 1]) return RSORT_ERR_ARG;
-    int bits = 1;
-    while ((1 << bits) < num_buckets) ++bits;
+    const int bits = partition_bits(num_buckets);
     const int pairs = d_vals_in != nullptr;
     rsort_plan p;
     int st = plan_fill(n, bits, pairs, 0, &p, /*partition=*/1);

@@ -196,9 +196,11 @@ struct Digit {
         if constexpr (DMODE == kDigitShift) {
             return (key >> shift) & ((1u << BITS) - 1u);
         } else {
+            // only 2^BITS - 1 splitters can exist (the host sizes BITS to the bucket count)
+            constexpr int NS = ((1 << BITS) - 1) < kMaxSplitters ? ((1 << BITS) - 1) : kMaxSplitters;
             uint32_t d = 0;
 #pragma unroll
-            for (int i = 0; i < kMaxSplitters; ++i) d += ((uint32_t)i < nsplit && key >= split[i]) ? 1u : 0u;
+            for (int i = 0; i < NS; ++i) d += ((uint32_t)i < nsplit && key >= split[i]) ? 1u : 0u;
             return d;
         }
     }
@@ -1037,8 +1039,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         inv = carry;
         g_run = g;
         // the invalid slots get a key of this digit (never stored: masked), so every staged
-        // slot's key tells the output phase its digit
-        for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = d_own << a.shift;
+        // slot's key tells the output phase its digit (a bucket's lower splitter in split mode;
+        // a bucket whose splitter repeats is empty and writes no line)
+        uint32_t ik = d_own << a.shift;
+        if constexpr (DMODE == kDigitSplit)
+            ik = (d_own == 0 || a.nsplit == 0) ? 0u : a.splitters[min(d_own, a.nsplit) - 1u];
+        for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = ik;
     }
 
     const uint32_t base = w * SEG + lane;
@@ -1431,6 +1437,14 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
     if (rank != kRankSplit && rank != kRankAtomic && rank != kRankCount) return nullptr;
     if (dmode == kDigitSplit) {
         if constexpr (BITS <= 4) {
+            if constexpr (BITS >= 2) {
+                // partition into 3..16 key ranges: whole lines from 4096-key tiles, like k = 3, 4
+                // (a digit's thread group must fit one wave: BITS >= 2)
+                constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
+                if (geom == kGeomSmall && rank == kRankAtomic && aligned16)
+                    return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
+                                                                      PAIRS, kDigitSplit, true, 0, PAIRS ? 0 : 3>);
+            }
             if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
         }
         return nullptr;

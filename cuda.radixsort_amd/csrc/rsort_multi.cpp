@@ -21,6 +21,8 @@ namespace {
 
 constexpr int kTopBits = 12;
 constexpr int kMaxRanks = kMaxSplitters + 1;
+// keys per RCCL message piece (512 MiB): 1 GiB messages arrive whole, 2 GiB ones do not
+constexpr unsigned long long kMaxMessage = 1ull << 27;
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -147,22 +149,33 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
     }
     if (n_recv > (unsigned long long)capacity) return RSORT_ERR_CAPACITY;
 
-    // 6: one exchange; chunks land in source-rank order (keeps pairs stable)
-    if ((st = nccl_status(ncclGroupStart()))) return st;
-    unsigned long long so = 0, ro = 0;
-    for (int r = 0; r < world; ++r) {
-        if (send[r]) {
-            ncclSend(m.part_k + so, send[r], ncclUint32, r, comm, s);
-            if (pairs) ncclSend(m.part_v + so, send[r], ncclUint32, r, comm, s);
+    // 6: the exchange; chunks land in source-rank order (keeps pairs stable). Every message is
+    // cut into pieces of at most kMaxMessage keys: this RCCL (2.26, ROCm 7) silently leaves the
+    // second half of a >= 2 GiB message unwritten (dev/a2a_lab.py), and with 2^30 keys per GPU
+    // two ranks exchange ~2 GiB each way. The piece count comes from the whole count matrix, so
+    // every rank runs the same number of groups.
+    unsigned long long biggest = 0;
+    for (int i = 0; i < world * world; ++i) biggest = std::max(biggest, all[i]);
+    const unsigned long long pieces = std::max(1ull, (biggest + kMaxMessage - 1) / kMaxMessage);
+    for (unsigned long long q = 0; q < pieces; ++q) {
+        if ((st = nccl_status(ncclGroupStart()))) return st;
+        unsigned long long so = 0, ro = 0;
+        for (int r = 0; r < world; ++r) {
+            const unsigned long long a0 = std::min(send[r], q * kMaxMessage), a1 = std::min(send[r], (q + 1) * kMaxMessage);
+            const unsigned long long b0 = std::min(recv[r], q * kMaxMessage), b1 = std::min(recv[r], (q + 1) * kMaxMessage);
+            if (a1 > a0) {
+                ncclSend(m.part_k + so + a0, a1 - a0, ncclUint32, r, comm, s);
+                if (pairs) ncclSend(m.part_v + so + a0, a1 - a0, ncclUint32, r, comm, s);
+            }
+            if (b1 > b0) {
+                ncclRecv(d_keys_out + ro + b0, b1 - b0, ncclUint32, r, comm, s);
+                if (pairs) ncclRecv(d_vals_out + ro + b0, b1 - b0, ncclUint32, r, comm, s);
+            }
+            so += send[r];
+            ro += recv[r];
         }
-        if (recv[r]) {
-            ncclRecv(d_keys_out + ro, recv[r], ncclUint32, r, comm, s);
-            if (pairs) ncclRecv(d_vals_out + ro, recv[r], ncclUint32, r, comm, s);
-        }
-        so += send[r];
-        ro += recv[r];
+        if ((st = nccl_status(ncclGroupEnd()))) return st;
     }
-    if ((st = nccl_status(ncclGroupEnd()))) return st;
 
     // 7: local sort of what arrived, in place
     if (n_recv > 0) {

@@ -8,7 +8,8 @@ BASELINE config 5 / SURVEY §8e. One process per GPU, torch.distributed over RCC
   3. splitters on bin edges balancing ~n/world keys per rank (host, 4096 values)
   4. stable partition of the local keys into world buckets (HIP: rsort_partition_device)
   5. all_to_all of the per-destination counts        (RCCL, world x i64)
-  6. all_to_all_single of the keys (and values)      (RCCL over xGMI: one peer per link)
+  6. all_to_all of the keys (and values)             (RCCL over xGMI: one peer per link;
+                                                      messages cut to <= 512 MiB pieces)
   7. local LSD sort of what arrived                   (HIP: the single-GPU sort)
 
 Rank r ends with the keys of global ranks [offset_r, offset_r + count_r); concatenating the
@@ -25,6 +26,12 @@ import torch
 import torch.distributed as dist
 
 import radixsort as rs
+
+# Keys per RCCL message (512 MiB of u32): the RCCL of this image (2.26, ROCm 7; torch 2.10)
+# silently leaves the second half of an all_to_all message of >= 2 GiB unwritten
+# (dev/a2a_lab.py: 1 GiB arrives whole, 2 GiB - 4 B does not), and two ranks holding 2^30 keys
+# each exchange ~2 GiB each way. Larger exchanges go in rounds of pieces this size.
+MAX_MESSAGE = 1 << 27
 
 
 class GpuOps:
@@ -94,16 +101,30 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12):
     if ops is None:
         ops = GpuOps(keys.device)
     dev = keys.device
-    host_comm = dist.get_backend(group) == "gloo" and dev.type != "cpu"
+    gloo = dist.get_backend(group) == "gloo"
+    host_comm = gloo and dev.type != "cpu"
     cdev = torch.device("cpu") if host_comm else dev
 
-    def a2a(out, inp, out_splits=None, in_splits=None):
-        if not host_comm:
-            dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
-            return out
-        o = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
-        out.copy_(o)
+    def a2a(out, inp, out_splits, in_splits, pieces):
+        """all_to_all of `inp` (segments in_splits, one per destination) into `out` (segments
+        out_splits, one per source), every message cut into `pieces` rounds of <= MAX_MESSAGE."""
+        so = np.concatenate([[0], np.cumsum(in_splits)]).astype(np.int64)
+        ro = np.concatenate([[0], np.cumsum(out_splits)]).astype(np.int64)
+        for q in range(pieces):
+            lo, hi = q * MAX_MESSAGE, (q + 1) * MAX_MESSAGE
+            ins = [inp[so[i] + min(lo, in_splits[i]):so[i] + min(hi, in_splits[i])] for i in range(world)]
+            outs = [out[ro[j] + min(lo, out_splits[j]):ro[j] + min(hi, out_splits[j])] for j in range(world)]
+            if not gloo:
+                dist.all_to_all(outs, ins, group=group)  # RCCL: grouped send/recv of the pieces
+                continue
+            # gloo (tests): one all_to_all_single of the round's pieces on host copies
+            o = torch.empty(sum(int(x.numel()) for x in outs), dtype=out.dtype)
+            dist.all_to_all_single(o, torch.cat([x.cpu() for x in ins]), output_split_sizes=[int(x.numel()) for x in outs],
+                                   input_split_sizes=[int(x.numel()) for x in ins], group=group)
+            off = 0
+            for x in outs:
+                x.copy_(o[off:off + x.numel()])
+                off += x.numel()
         return out
 
     # 1-3: global histogram of the top bits -> splitters
@@ -123,14 +144,18 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12):
     dist.all_to_all_single(recv_t, send_t, group=group)
     recv = recv_t.cpu().numpy()
 
-    # 6: exchange keys (and values); chunks arrive in source-rank order (stability)
+    # 6: exchange keys (and values); chunks arrive in source-rank order (stability). Every rank
+    # needs the same number of rounds: the largest message anywhere, by one small all_reduce.
     n_recv = int(recv.sum())
+    big = torch.tensor([int(max(send.max(), recv.max()))], dtype=torch.int64, device=cdev)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
+    pieces = max(1, -(-int(big.item()) // MAX_MESSAGE))
     rk = torch.empty(n_recv, dtype=keys.dtype, device=dev)
-    a2a(rk, pk, recv.tolist(), send.tolist())
+    a2a(rk, pk, recv.tolist(), send.tolist(), pieces)
     rv = None
     if vals is not None:
         rv = torch.empty(n_recv, dtype=vals.dtype, device=dev)
-        a2a(rv, pv, recv.tolist(), send.tolist())
+        a2a(rv, pv, recv.tolist(), send.tolist(), pieces)
 
     # 7: local LSD sort of the received bucket
     ok, ov = ops.sort(rk, rv, k_bits)

@@ -170,3 +170,48 @@ def test_c_multi_two_ranks_one_gpu(tmp_path):
     rk, rv = oracle_sort_pairs(np.concatenate(all_k), np.concatenate(all_v), 8)
     assert np.array_equal(np.concatenate(got), rk)
     assert np.array_equal(np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)]), rv)
+
+
+# ------------------------------------------------------------------ >= 2 GiB exchange messages
+def _sorted_ref(d_keys):
+    return torch.sort(d_keys.to(torch.int64) & 0xFFFFFFFF)[0]
+
+
+def test_dist_sort_rccl_2gib_message():
+    """One rank sending itself 2^29 + 3 keys (a 2 GiB message): this RCCL leaves the second half
+    of such a message unwritten, so multi.py exchanges it in rounds of <= 512 MiB pieces."""
+    sys.path.insert(0, str(PKG))
+    import multi
+    import radixsort as rs
+    torch.cuda.set_device(0)
+    n = (1 << 29) + 3
+    with tempfile.TemporaryDirectory() as td:
+        store = dist.FileStore(os.path.join(td, "store"), 1)
+        dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        try:
+            keys = rs.empty_u32(n)
+            rs.gen_uniform(keys, 77)
+            ok, _, off = multi.dist_sort(keys, 8)
+            torch.cuda.synchronize()
+            assert off == 0 and ok.numel() == n
+            assert torch.equal(ok.to(torch.int64) & 0xFFFFFFFF, _sorted_ref(keys))
+        finally:
+            dist.destroy_process_group()
+
+
+def test_c_multi_2gib_message():
+    """rsort_u32_multi at one rank with a 2 GiB self message: grouped send/recv in pieces."""
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    torch.cuda.set_device(0)
+    n = (1 << 29) + 5
+    comm = rs.RcclComm(1, 0, rs.rccl_unique_id())
+    try:
+        keys = rs.empty_u32(n)
+        rs.gen_uniform(keys, 78)
+        ok, _, off = rs.multi_sort_device(comm, keys, 8)
+        torch.cuda.synchronize()
+        assert off == 0 and ok.numel() == n
+        assert torch.equal(ok.to(torch.int64) & 0xFFFFFFFF, _sorted_ref(keys))
+    finally:
+        comm.close()

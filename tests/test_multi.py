@@ -66,8 +66,10 @@ def _inputs(rank, n, dist_name, pairs):
     return keys, vals
 
 
-def _worker(rank, world, port, n, dist_name, pairs, out_dir):
+def _worker(rank, world, port, n, dist_name, pairs, out_dir, max_message=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if max_message:
+        multi.MAX_MESSAGE = max_message  # exchange in several rounds of pieces
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         keys, vals = _inputs(rank, n, dist_name, pairs)
@@ -86,12 +88,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,dist_name,pairs", [(2, "uniform", False), (2, "zipf", True),
-                                                   (4, "uniform", True), (4, "skewed", False),
-                                                   (3, "zipf", False)])
-def test_dist_sort_gloo(tmp_path, world, dist_name, pairs):
+@pytest.mark.parametrize("world,dist_name,pairs,max_message", [(2, "uniform", False, None), (2, "zipf", True, None),
+                                                               (4, "uniform", True, None), (4, "skewed", False, None),
+                                                               (3, "zipf", False, None), (3, "uniform", True, 1000),
+                                                               (2, "skewed", False, 777)])
+def test_dist_sort_gloo(tmp_path, world, dist_name, pairs, max_message):
+    """max_message: pieces per message in the exchange (multi.MAX_MESSAGE, 2^27 keys by default,
+    works around RCCL dropping the second half of >= 2 GiB messages): small values force rounds."""
     n = 50_000
-    mp.spawn(_worker, args=(world, _free_port(), n, dist_name, pairs, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, dist_name, pairs, str(tmp_path), max_message), nprocs=world,
+             join=True)
     all_k, all_v = zip(*[_inputs(r, n, dist_name, pairs) for r in range(world)])
     keys = np.concatenate(all_k)
     got = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
