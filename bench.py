@@ -150,6 +150,14 @@ def primitives(a, dev):
         f"{rs.scatter_kernel_name(p)}: block-local rank + global scatter")
     row("local_sort", timed(lambda: rs.pass_local_sort(p, keys, out, 0)), 8 * n,
         "block-local stable sort of every tile (sortLocallyDataBlocks' result)")
+    for nb in (1, 2, 8):
+        # the multi-GPU step's stable partition into nb key ranges (uniform splitters)
+        spl = [(i << 32) // nb for i in range(1, nb)]
+        starts = torch.empty(nb + 1, dtype=torch.int32, device=dev)
+        pws = rs.workspace(int(rs._lib().rsort_partition_workspace_size(n, nb, 0)), dev)
+        row(f"partition_{nb}", timed(lambda: rs.partition_device(keys, out, spl, starts, ws=pws)), 12 * n,
+            f"rsort_partition_device into {nb} key ranges (histogram 4n + scatter 8n bytes)")
+        del pws
     print(json.dumps({"primitives": rows, "keys": n, "k_bits": k, "tile_keys": p.tile_keys,
                       "num_chunks": p.num_chunks, "steps": a.steps, "peak_GBs": HBM_PEAK_GBS}), flush=True)
 
@@ -170,6 +178,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or a.dist_path
+    if os.environ.get("NCCL_DEBUG", "").upper() == "VERSION":
+        os.environ["NCCL_DEBUG"] = "WARN"  # RCCL's version banner would share rank 0's stdout with the JSON line
     if use_dist:
         import torch.distributed as dist
         if world == 1:

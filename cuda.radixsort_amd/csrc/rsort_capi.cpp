@@ -96,8 +96,10 @@ int device_cus() {
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
 // CU two large tiles.
 int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
-    if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
+    // partitions: 4096-key tiles (measured at 2^30 keys into 8 ranges: 1024-thread 16384-key
+    // tiles need 4-bit bucket digits, i.e. 15 splitter compares per key, and were 1.3x slower)
+    if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
@@ -134,7 +136,9 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     const int64_t tiles = std::max<int64_t>(1, (n + tile - 1) / tile);
     if (tpc == 0) {
         // one resident wave of workgroups: as many chunks as the scatter kernel keeps resident
-        int bpc = cus > 0 ? scatter_blocks_per_cu(k, pairs, internal_rank(partition ? RSORT_RANK_MATCH : rank), geom) : 0;
+        // (of the kernel this plan's scatter runs: a partition's digit is a bucket)
+        int bpc = cus > 0 ? scatter_blocks_per_cu(k, pairs, internal_rank(partition ? RSORT_RANK_MATCH : rank), geom,
+                                                  partition ? kDigitSplit : kDigitShift) : 0;
         if (bpc <= 0) bpc = 2;
         const int64_t target = std::max<int64_t>(1, (int64_t)(cus > 0 ? cus : 256) * bpc);
         tpc = (tiles + target - 1) / target;
@@ -157,11 +161,13 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     return RSORT_OK;
 }
 
-// Digit bits of a partition into num_buckets key ranges: at least 2, so that the whole-line
-// scatter kernel (a digit's threads inside one wave) takes it.
-int partition_bits(int num_buckets) {
-    int bits = 2;
-    while ((1 << bits) < num_buckets) ++bits;
+// Digit bits of a partition of n keys into num_buckets key ranges: enough for the buckets, and
+// enough that the whole-line scatter kernel of the partition's tile shape (choose_geom) gives
+// each digit at most one wave of threads.
+int partition_bits(int64_t n, int num_buckets, int pairs) {
+    const int geom = choose_geom(n, 0, pairs, RSORT_RANK_MATCH, 1, device_cus());
+    int bits = 1;
+    while ((1 << bits) < num_buckets || (kGeomShape[geom].threads >> bits) > kWave) ++bits;
     return bits;
 }
 
@@ -639,7 +645,7 @@ int rsort_profile_end(rsort_phase_times *out) {
 
 size_t rsort_partition_workspace_size(int64_t n, int num_buckets, int pairs) {
     if (num_buckets < 1 || num_buckets > kMaxSplitters + 1) return 0;
-    const int bits = partition_bits(num_buckets);
+    const int bits = partition_bits(n, num_buckets, pairs);
     rsort_plan p;
     if (plan_fill(n, bits, pairs, 0, &p, /*partition=*/1) != RSORT_OK) return 0;
     return p.workspace_bytes;
@@ -653,8 +659,8 @@ int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
     if (num_buckets > 1 && !splitters) return RSORT_ERR_ARG;
     for (int i = 1; i + 1 < num_buckets; ++i)
         if (splitters[i] < splitters[i - 1]) return RSORT_ERR_ARG;
-    const int bits = partition_bits(num_buckets);
     const int pairs = d_vals_in != nullptr;
+    const int bits = partition_bits(n < 0 ? 0 : n, num_buckets, pairs);
     rsort_plan p;
     int st = plan_fill(n, bits, pairs, 0, &p, /*partition=*/1);
     if (st) return st;

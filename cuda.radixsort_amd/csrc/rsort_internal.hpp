@@ -134,6 +134,6 @@ hipError_t launch_gen_zipf(uint32_t *out, uint64_t n, uint64_t seed, const uint3
 hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t s);
 hipError_t launch_widen(const uint32_t *in, unsigned long long *out, uint32_t n, hipStream_t s);
 // Resident scatter workgroups per CU (occupancy query), 0 on error.
-int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom);
+int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmode = kDigitShift);
 
 }  // namespace rsort

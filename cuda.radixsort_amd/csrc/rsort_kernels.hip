@@ -119,6 +119,37 @@ __device__ __forceinline__ uint32_t group_lane(uint32_t x, uint32_t q) {
     }
 }
 
+// Exclusive prefix (pre) of x over the lanes of this lane's aligned group of TPD lanes below it
+// (sub = lane % TPD) and the group's total. Small groups: one group_lane per member; groups of
+// 16..64 lanes: the DPP row scan of wave_incl_scan cut to the group, plus one bpermute for the
+// total. Every lane of the wave must call it.
+template <uint32_t TPD>
+__device__ __forceinline__ void group_scan(uint32_t x, uint32_t sub, uint32_t &pre, uint32_t &tot) {
+    if constexpr (TPD <= 8) {
+        pre = 0;
+        tot = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < TPD; ++q) {
+            const uint32_t y = group_lane<TPD>(x, q);
+            if (q < sub) pre += y;
+            tot += y;
+        }
+    } else {
+        static_assert(TPD == 16 || TPD == 32 || TPD == 64, "groups of 16, 32 or 64 lanes");
+        uint32_t v = x;
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+        if constexpr (TPD >= 32)
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+        if constexpr (TPD == 64)
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+        pre = v - x;
+        tot = (uint32_t)__shfl((int)v, (int)((lane_id() & ~(TPD - 1u)) + TPD - 1u));
+    }
+}
+
 // Mask (lo, hi halves) of the lanes of this wave whose BITS-bit digit equals this lane's:
 // AND over bits b of (ballot(bit b) XNOR my bit b), one v_bitop3 per half per bit
 // (truth table 0x90 = a & ~(b ^ c) with a = mask, b = ballot half, c = my bit as 0 / ~0).
@@ -200,7 +231,10 @@ struct Digit {
             constexpr int NS = ((1 << BITS) - 1) < kMaxSplitters ? ((1 << BITS) - 1) : kMaxSplitters;
             uint32_t d = 0;
 #pragma unroll
-            for (int i = 0; i < NS; ++i) d += ((uint32_t)i < nsplit && key >= split[i]) ? 1u : 0u;
+            for (int i = 0; i < NS; ++i) {
+                if ((uint32_t)i >= nsplit) break;  // uniform: a scalar branch, not per-lane selects
+                d += key >= split[i] ? 1u : 0u;
+            }
             return d;
         }
     }
@@ -1127,6 +1161,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         // RF (rank first): the returning add IS the key's rank among its wave's keys of that digit
         // (lane order, kRankAtomic); two ranks (< 2^16) per register
         uint32_t rk[RF ? (KPT + 1) / 2 : 1];
+        // split digits (a compare per splitter) are kept from step 1, 4 bits each, for step 3
+        constexpr bool PD = DMODE == kDigitSplit && BITS <= 4;
+        uint32_t dpk[PD ? (KPT + 7) / 8 : 1];
+#pragma unroll
+        for (int i = 0; i < (PD ? (KPT + 7) / 8 : 1); ++i) dpk[i] = 0;
         uint32_t nkey[KPT];
         uint32_t nval[PAIRS ? KPT : 1];
         if (full) {
@@ -1135,17 +1174,22 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 if constexpr (RF) {
                     // (ABL & 4: dev/scatter_lab ablation -- plain lane-ordered adds, no aggregation;
                     // measured: aggregation is ~2% faster even on uniform keys, 1.7x on clustered)
-                    const uint32_t r = (ABL & 4) ? atomicAdd(&s_cnt[w * R + dig(key[j])], 1u)
-                                                 : rank_add(&s_cnt[w * R], dig(key[j]));
+                    const uint32_t dj = dig(key[j]);
+                    if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
+                    const uint32_t r = (ABL & 4) ? atomicAdd(&s_cnt[w * R + dj], 1u)
+                                                 : rank_add(&s_cnt[w * R], dj);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 } else {
-                    count_add(&s_cnt[w * R], dig(key[j]));
+                    const uint32_t dj = dig(key[j]);
+                    if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
+                    count_add(&s_cnt[w * R], dj);
                 }
             }
         } else {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = dig(key[j]);
+                if constexpr (PD) dpk[j / 8] |= d << (4 * (j % 8));
                 uint32_t r = 0;
                 if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
                 if constexpr (RF) rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
@@ -1171,13 +1215,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         }
         // exclusive prefix of the parts inside the group and the digit's tile count (the group is
         // TPD consecutive lanes of one wave)
-        uint32_t gpre = 0, cnt = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < TPD; ++q) {
-            const uint32_t y = group_lane<TPD>(part, q);
-            if (q < sub) gpre += y;
-            cnt += y;
-        }
+        uint32_t gpre, cnt;
+        group_scan<TPD>(part, sub, gpre, cnt);
         uint32_t wcnt = 0, A = 0, e = 0;
         RS_STAMP(1);
         if (leader) {
@@ -1282,7 +1321,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             for (int u = 0; u < SB; ++u) {
                 const int j = j0 + u;
                 asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
-                dd[u] = dig(key[j]);
+                if constexpr (PD) dd[u] = (dpk[j / 8] >> (4 * (j % 8))) & 15u;
+                else dd[u] = dig(key[j]);
                 if constexpr (RF) {
                     const uint32_t bl = s_cnt[w * R + dd[u]];
                     pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
@@ -1604,9 +1644,9 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     return hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
 }
 
-int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom) {
+int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmode) {
     if (geom < 0 || geom >= kGeomCount) return 0;
-    void *fn = scatter_kernel(bits, pairs, rank_algo, kDigitShift, geom, 1);
+    void *fn = scatter_kernel(bits, pairs, rank_algo, dmode, geom, 1);
     if (!fn) return 0;
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kGeomShape[geom].threads, 0) != hipSuccess)
