@@ -178,8 +178,6 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or a.dist_path
-    if os.environ.get("NCCL_DEBUG", "").upper() == "VERSION":
-        os.environ["NCCL_DEBUG"] = "WARN"  # RCCL's version banner would share rank 0's stdout with the JSON line
     if use_dist:
         import torch.distributed as dist
         if world == 1:

@@ -702,6 +702,18 @@ int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits, uint32_
     return hip_status(launch_diff_starts(c.starts, (uint32_t)p.bins, d_hist, s));
 }
 
+int rsort_top_histogram_sampled(const uint32_t *d_keys, int64_t n, int top_bits, int stride, uint32_t *d_hist,
+                                void *stream) {
+    if (top_bits < 1 || top_bits > kMaxBits) return RSORT_ERR_BITS;
+    if (n < 0 || n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (stride < 1 || !d_hist || (n > 0 && !d_keys)) return RSORT_ERR_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(d_hist, 0, ((size_t)1 << top_bits) * 4, s) != hipSuccess) return RSORT_ERR_HIP;
+    if (n == 0) return RSORT_OK;
+    PhaseScope ps(RSORT_PHASE_HISTOGRAM, (n + stride - 1) / stride, s);
+    return hip_status(launch_top_hist_sampled(d_keys, (uint64_t)n, (uint32_t)top_bits, (uint32_t)stride, d_hist, s));
+}
+
 int rsort_gen_uniform(uint32_t *d_out, int64_t n, uint64_t seed, void *stream) {
     if (n < 0) return RSORT_ERR_SIZE;
     if (n == 0) return RSORT_OK;

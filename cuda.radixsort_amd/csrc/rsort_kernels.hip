@@ -1372,6 +1372,25 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     RS_STAMP_FLUSH();
 }
 
+// Top-bits histogram of every stride-th 256-key block (the multi-GPU sort's splitter sample):
+// one block per workgroup iteration, 2^top_bits LDS counters, added into the zeroed hist.
+__global__ __launch_bounds__(256) void rs_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits,
+                                                           uint32_t stride, uint32_t *hist) {
+    __shared__ uint32_t s_h[1u << 12];
+    const uint32_t t = threadIdx.x;
+    const uint32_t bins = 1u << top_bits;
+    for (uint32_t i = t; i < bins; i += 256) s_h[i] = 0;
+    __syncthreads();
+    const uint64_t nblk = (n + 255) / 256;
+    for (uint64_t b = (uint64_t)blockIdx.x * stride; b < nblk; b += (uint64_t)gridDim.x * stride) {
+        const uint64_t i = b * 256 + t;
+        if (i < n) count_add(s_h, keys[i] >> (32 - top_bits));
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < bins; i += 256)
+        if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
+}
+
 __global__ void rs_gather_starts(const uint32_t *table, uint32_t num_chunks, uint32_t bins,
                                  uint64_t n, uint32_t *starts) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1692,6 +1711,14 @@ hipError_t launch_diff_starts(const uint32_t *starts, uint32_t bins, uint32_t *h
 static unsigned gen_grid(uint64_t n) {
     const uint64_t g = (n + 255) / 256;
     return (unsigned)(g < 65536 ? (g ? g : 1) : 65536);
+}
+
+hipError_t launch_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits, uint32_t stride,
+                                   uint32_t *hist, hipStream_t s) {
+    const uint64_t blocks = ((n + 255) / 256 + stride - 1) / stride;  // sampled blocks
+    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>(blocks / 16, 1), 2048);
+    rs_top_hist_sampled<<<grid, 256, 0, s>>>(keys, n, top_bits, stride, hist);
+    return hipGetLastError();
 }
 
 hipError_t launch_gen_uniform(uint32_t *out, uint64_t n, uint64_t seed, hipStream_t s) {

@@ -20,6 +20,8 @@ using namespace rsort;
 namespace {
 
 constexpr int kTopBits = 12;
+// splitters come from every 16th block of 256 keys: their balance only sets the load per rank
+constexpr int kSampleStride = 16;
 constexpr int kMaxRanks = kMaxSplitters + 1;
 // keys per RCCL message piece (512 MiB): 1 GiB messages arrive whole, 2 GiB ones do not
 constexpr unsigned long long kMaxMessage = 1ull << 27;
@@ -113,7 +115,7 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
     int st;
 
     // 1-3: global top-bits histogram -> splitters (host)
-    if ((st = rsort_top_histogram(d_keys, n, kTopBits, m.hist32, m.sub, m.sub_bytes, stream))) return st;
+    if ((st = rsort_top_histogram_sampled(d_keys, n, kTopBits, kSampleStride, m.hist32, stream))) return st;
     if (launch_widen(m.hist32, m.hist64, 1u << kTopBits, s) != hipSuccess) return RSORT_ERR_HIP;
     if ((st = nccl_status(ncclAllReduce(m.hist64, m.hist64, (size_t)1 << kTopBits, ncclUint64, ncclSum, comm, s))))
         return st;

@@ -3,7 +3,7 @@
 No reference counterpart (the reference is single-GPU, Parallel7.cu:10/:697); this is
 BASELINE config 5 / SURVEY §8e. One process per GPU, torch.distributed over RCCL ("nccl"):
 
-  1. top-bits histogram of the local keys            (HIP: rsort_top_histogram)
+  1. top-bits histogram of a 1/16 block sample       (HIP: rsort_top_histogram_sampled)
   2. all_reduce(SUM) of the 2^top_bits counts        (RCCL, 16 KiB)
   3. splitters on bin edges balancing ~n/world keys per rank (host, 4096 values)
   4. stable partition of the local keys into world buckets (HIP: rsort_partition_device)
@@ -32,6 +32,9 @@ import radixsort as rs
 # (dev/a2a_lab.py: 1 GiB arrives whole, 2 GiB - 4 B does not), and two ranks holding 2^30 keys
 # each exchange ~2 GiB each way. Larger exchanges go in rounds of pieces this size.
 MAX_MESSAGE = 1 << 27
+# Splitters come from the top-bits histogram of every 16th block of 256 keys (all ranks sample
+# alike, so the global histogram keeps its proportions; a 2^30-key rank reads 256 MiB, not 4 GiB).
+SAMPLE_STRIDE = 16
 
 
 class GpuOps:
@@ -46,9 +49,12 @@ class GpuOps:
             self._ws = rs.workspace(nbytes, self.device)
         return self._ws
 
-    def top_histogram(self, keys, top_bits):
+    def top_histogram(self, keys, top_bits, stride=1):
         h = torch.empty(1 << top_bits, dtype=torch.int32, device=self.device)
-        rs.top_histogram(keys, top_bits, h, ws=self._workspace(rs.workspace_size(keys.numel(), top_bits)))
+        if stride > 1:
+            rs.top_histogram_sampled(keys, top_bits, stride, h)
+        else:
+            rs.top_histogram(keys, top_bits, h, ws=self._workspace(rs.workspace_size(keys.numel(), top_bits)))
         return h
 
     def partition(self, keys, vals, splitters):
@@ -127,8 +133,9 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12):
                 off += x.numel()
         return out
 
-    # 1-3: global histogram of the top bits -> splitters
-    h = ops.top_histogram(keys, top_bits).to(torch.int64).to(cdev)
+    # 1-3: global histogram of the top bits (of a 1/SAMPLE_STRIDE block sample: the splitters
+    # only set each rank's load) -> splitters
+    h = ops.top_histogram(keys, top_bits, SAMPLE_STRIDE).to(torch.int64).to(cdev)
     dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
     hist = h.cpu().numpy()
     splitters = choose_splitters(hist, world, top_bits)

@@ -111,6 +111,7 @@ SIGNATURES = {
     "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
     "rsort_partition_device": ([_vp, _vp, _vp, _vp, _i64, _u32p, _int, _vp, _vp, _sz, _vp], _int),
     "rsort_top_histogram": ([_vp, _i64, _int, _vp, _vp, _sz, _vp], _int),
+    "rsort_top_histogram_sampled": ([_vp, _i64, _int, _int, _vp, _vp], _int),
     "rsort_multi_workspace_size": ([_i64, _i64, _int, _int, _int], _sz),
     "rsort_u32_multi": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int, _vp,
                          _vp, _sz, _vp], _int),
@@ -442,6 +443,12 @@ def partition_device(keys_in, keys_out, splitters, bucket_starts, vals_in=None, 
     _check(_lib().rsort_partition_device(_ptr(keys_in), _ptr(vals_in), _ptr(keys_out), _ptr(vals_out), n, sp, nb,
                                          _ptr(bucket_starts), _ptr(ws), ws.numel(), _stream(stream)),
            "rsort_partition_device")
+
+
+def top_histogram_sampled(keys, top_bits, stride, hist, stream=None):
+    """Top-bits histogram of every `stride`-th 256-key block (rsort_top_histogram_sampled)."""
+    _check(_lib().rsort_top_histogram_sampled(_ptr(keys), keys.numel(), int(top_bits), int(stride), _ptr(hist),
+                                              _stream(stream)), "rsort_top_histogram_sampled")
 
 
 def top_histogram(keys, top_bits, hist, ws=None, stream=None):

@@ -202,6 +202,11 @@ RSORT_API int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *
 RSORT_API int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits,
                                   uint32_t *d_hist, void *d_workspace, size_t workspace_bytes,
                                   void *stream);
+/* The same histogram over a sample: the keys of every `stride`-th block of 256 (block b is
+ * counted iff b % stride == 0; stride 1 = every key). No workspace. The multi-GPU sort chooses
+ * its splitters from this (stride 16: a sixteenth of the keys read). */
+RSORT_API int rsort_top_histogram_sampled(const uint32_t *d_keys, int64_t n, int top_bits,
+                                          int stride, uint32_t *d_hist, void *stream);
 
 /* ---------------------------------------------------------------- multi-GPU sort (RCCL) */
 /* One rank per GPU over an RCCL communicator (`nccl_comm` is an ncclComm_t; the

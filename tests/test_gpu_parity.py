@@ -321,6 +321,18 @@ def test_top_histogram():
     assert np.array_equal(host(h), np.bincount(x >> np.uint32(20), minlength=4096).astype(np.uint32))
 
 
+@pytest.mark.parametrize("n,stride,bits", [(300001, 1, 12), (300001, 16, 12), (1 << 22, 16, 12),
+                                            (1000, 7, 5), (0, 16, 12), (5 << 20, 3, 8)])
+def test_top_histogram_sampled(n, stride, bits):
+    """rsort_top_histogram_sampled = numpy's bincount over every stride-th 256-key block."""
+    x = zipf_keys(n, seed=n + stride) if n else np.zeros(0, np.uint32)
+    h = rs.empty_u32(1 << bits)
+    rs.top_histogram_sampled(dev(x) if n else rs.empty_u32(0), bits, stride, h)
+    torch.cuda.synchronize()
+    sample = x[(np.arange(n) // 256) % stride == 0]
+    assert np.array_equal(host(h), np.bincount(sample >> np.uint32(32 - bits), minlength=1 << bits).astype(np.uint32))
+
+
 @pytest.mark.parametrize("nb", [1, 2, 3, 8, 16])
 def test_partition_stable(nb):
     n = 200003

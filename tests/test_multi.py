@@ -37,9 +37,11 @@ def _t(a):
 class NumpyOps:
     """CPU stand-in for multi.GpuOps with the kernels' exact semantics (test-only)."""
 
-    def top_histogram(self, keys, top_bits):
-        return torch.from_numpy(np.bincount(_u32(keys) >> np.uint32(32 - top_bits),
-                                            minlength=1 << top_bits).astype(np.int32))
+    def top_histogram(self, keys, top_bits, stride=1):
+        k = _u32(keys)
+        if stride > 1:  # rsort_top_histogram_sampled: every stride-th block of 256 keys
+            k = k[(np.arange(k.size) // 256) % stride == 0]
+        return torch.from_numpy(np.bincount(k >> np.uint32(32 - top_bits), minlength=1 << top_bits).astype(np.int32))
 
     def partition(self, keys, vals, splitters):
         k = _u32(keys)
@@ -110,9 +112,9 @@ def test_dist_sort_gloo(tmp_path, world, dist_name, pairs, max_message):
         assert np.array_equal(np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)]), rv)
     else:
         assert np.array_equal(np.concatenate(got), oracle_sort(keys, 8))
-    if dist_name == "uniform":  # splitters balance within a couple of top-bits bins
+    if dist_name == "uniform":  # splitters (from a 1/16 block sample) balance within a few percent
         sizes = np.array([g.size for g in got])
-        assert np.abs(sizes - keys.size / world).max() < 0.02 * keys.size
+        assert np.abs(sizes - keys.size / world).max() < 0.05 * keys.size
 
 
 def test_choose_splitters():
