@@ -1373,21 +1373,22 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 }
 
 // Top-bits histogram of every stride-th 256-key block (the multi-GPU sort's splitter sample):
-// one block per workgroup iteration, 2^top_bits LDS counters, added into the zeroed hist.
-__global__ __launch_bounds__(256) void rs_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits,
-                                                           uint32_t stride, uint32_t *hist) {
+// 1024 threads take four sampled blocks per iteration into 2^top_bits LDS counters, then add
+// them into the zeroed hist (one workgroup per CU keeps that final add to 2^top_bits per CU).
+__global__ __launch_bounds__(1024) void rs_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits,
+                                                            uint32_t stride, uint32_t *hist) {
     __shared__ uint32_t s_h[1u << 12];
     const uint32_t t = threadIdx.x;
     const uint32_t bins = 1u << top_bits;
-    for (uint32_t i = t; i < bins; i += 256) s_h[i] = 0;
+    for (uint32_t i = t; i < bins; i += 1024) s_h[i] = 0;
     __syncthreads();
-    const uint64_t nblk = (n + 255) / 256;
-    for (uint64_t b = (uint64_t)blockIdx.x * stride; b < nblk; b += (uint64_t)gridDim.x * stride) {
-        const uint64_t i = b * 256 + t;
+    const uint64_t nsb = ((n + 255) / 256 + stride - 1) / stride;  // sampled blocks
+    for (uint64_t sb = (uint64_t)blockIdx.x * 4 + t / 256; sb < nsb; sb += (uint64_t)gridDim.x * 4) {
+        const uint64_t i = sb * stride * 256 + (t % 256);
         if (i < n) count_add(s_h, keys[i] >> (32 - top_bits));
     }
     __syncthreads();
-    for (uint32_t i = t; i < bins; i += 256)
+    for (uint32_t i = t; i < bins; i += 1024)
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
@@ -1716,8 +1717,8 @@ static unsigned gen_grid(uint64_t n) {
 hipError_t launch_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits, uint32_t stride,
                                    uint32_t *hist, hipStream_t s) {
     const uint64_t blocks = ((n + 255) / 256 + stride - 1) / stride;  // sampled blocks
-    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>(blocks / 16, 1), 2048);
-    rs_top_hist_sampled<<<grid, 256, 0, s>>>(keys, n, top_bits, stride, hist);
+    const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>(blocks / 16, 1), 256);
+    rs_top_hist_sampled<<<grid, 1024, 0, s>>>(keys, n, top_bits, stride, hist);
     return hipGetLastError();
 }
 
