@@ -1503,7 +1503,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
                 constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
                 if (geom == kGeomSmall && rank == kRankAtomic && aligned16)
                     return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
-                                                                      PAIRS, kDigitSplit, true, 0, PAIRS ? 0 : 3>);
+                                                                      PAIRS, kDigitSplit, true, 0, PAIRS ? 2 : 3>);
             }
             if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
         }
@@ -1526,13 +1526,14 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
     if constexpr (BITS >= 5 && BITS <= 8) {
         if (geom == kGeomLarge) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomLarge>(rank);
         // whole-line stores need lane-ordered atomics and 16-B aligned outputs; else the same
-        // tiles through rs_scatter
+        // tiles through rs_scatter. Non-temporal (NT): keys-only loads and stores; pairs stores
+        // only (dev/scatter_lab LAB_PAIRS, 2^30: 4.24 -> 3.96 ms; nt loads 4.66 ms)
         constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
         if (geom == GL) {
             if (rank == kRankAtomic && aligned16)
                 return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
                                                                   PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
-                                                                  kDigitShift, true, 0, PAIRS ? 0 : 3>);
+                                                                  kDigitShift, true, 0, PAIRS ? 2 : 3>);
             return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }
