@@ -254,6 +254,13 @@ int main(int argc, char **argv) {
         lines<2, 256, 16, 32, false, true, 0, 3>(c, "k2 256x16 lines32 nt", 1.0);
         return 0;
     }
+    if (getenv("LAB_SHAPE")) {  // keys-only line kernel: 16384-key tiles as 1024x16 or 512x32
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
+        lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt", 1.0);
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt again", 1.0);
+        lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt again", 1.0);
+        return 0;
+    }
     if (getenv("LAB_PAIRS")) {  // key+value line kernel: non-temporal loads / stores
         lines<8, 512, 16, 16, true, true, 0, 0>(c, "k8 pairs 512x16 lines16", 1.0);
         lines<8, 512, 16, 16, true, true, 0, 1>(c, "k8 pairs 512x16 lines16 ntload", 1.0);
