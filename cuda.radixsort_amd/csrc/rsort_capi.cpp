@@ -101,6 +101,9 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     // tiles need 4-bit bucket digits, i.e. 15 splitter compares per key, and were 1.3x slower)
     if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
+    // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:
+    // 1.61 ms per pass against 1.75 ms with 4096-key tiles; at 2^26 0.120 against 0.113)
+    if (k == 4 && !pairs && n >= ((int64_t)1 << 28)) return kGeomLines;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
     // lines: 2^26 keys, k = 4: 0.117 vs 0.144 ms per pass, dev/scatter_lab.hip); k <= 2 keeps

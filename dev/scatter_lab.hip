@@ -246,6 +246,8 @@ int main(int argc, char **argv) {
         lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt", 1.0);
         lines<4, 256, 16, 32, false, true, 0, 1>(c, "k4 256x16 lines32 ntload", 1.0);
         lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt again", 1.0);
+        lines<4, 1024, 16, 32, false, true, 0, 3>(c, "k4 1024x16 lines32 nt", 1.0);
+        lines<4, 1024, 16, 32, false, true, 0, 3>(c, "k4 1024x16 lines32 nt again", 1.0);
         c.have_ref = false;
         variant<3, 512, 16, false, kRankAtomic, 4>(c, "k3 512x16 atomic w4 (lib)", 1.0);
         lines<3, 256, 16, 32, false, true, 0, 3>(c, "k3 256x16 lines32 nt", 1.0);

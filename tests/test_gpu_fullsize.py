@@ -33,7 +33,7 @@ def is_sorted(t):
     return bool((x[1:] >= x[:-1]).all())
 
 
-@pytest.mark.parametrize("n,k", [(1 << 26, 4), (1 << 30, 8)])
+@pytest.mark.parametrize("n,k", [(1 << 26, 4), (1 << 30, 8), ((1 << 28) + 77, 4), ((1 << 27) - 3, 3)])
 def test_fullsize_uniform(n, k):
     keys = rs.empty_u32(n)
     rs.gen_uniform(keys, 0x5EED)
