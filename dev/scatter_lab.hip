@@ -263,6 +263,13 @@ int main(int argc, char **argv) {
         lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt again", 1.0);
         return 0;
     }
+    if (getenv("LAB_PAIRS2")) {  // key+value line kernel shape: 512 x 16 or 1024 x 8 (nt stores)
+        lines<8, 512, 16, 16, true, true, 0, 2>(c, "k8 pairs 512x16 lines16 ntstore", 1.0);
+        lines<8, 1024, 8, 16, true, true, 0, 2>(c, "k8 pairs 1024x8 lines16 ntstore", 1.0);
+        lines<8, 512, 16, 16, true, true, 0, 2>(c, "k8 pairs 512x16 lines16 ntstore again", 1.0);
+        lines<8, 1024, 8, 16, true, true, 0, 2>(c, "k8 pairs 1024x8 lines16 ntstore again", 1.0);
+        return 0;
+    }
     if (getenv("LAB_PAIRS")) {  // key+value line kernel: non-temporal loads / stores
         lines<8, 512, 16, 16, true, true, 0, 0>(c, "k8 pairs 512x16 lines16", 1.0);
         lines<8, 512, 16, 16, true, true, 0, 1>(c, "k8 pairs 512x16 lines16 ntload", 1.0);
