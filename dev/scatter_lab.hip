@@ -256,6 +256,15 @@ int main(int argc, char **argv) {
         lines<2, 256, 16, 32, false, true, 0, 3>(c, "k2 256x16 lines32 nt", 1.0);
         return 0;
     }
+    if (getenv("LAB_P1")) {  // keys as pass 1 sees them: pass 0's output, then a pass on digit 1
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 0)", 1.0);
+        CK(hipMemcpy(c.keys, c.out, c.n * 4, hipMemcpyDeviceToDevice));
+        c.have_ref = false;
+        printf("input: pass-0 output\n");
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 1)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 1) again", 1.0, 8);
+        return 0;
+    }
     if (getenv("LAB_SHAPE")) {  // keys-only line kernel: 16384-key tiles as 1024x16 or 512x32
         lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
         lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt", 1.0);
