@@ -93,7 +93,8 @@ def _free_port():
 @pytest.mark.parametrize("world,dist_name,pairs,max_message", [(2, "uniform", False, None), (2, "zipf", True, None),
                                                                (4, "uniform", True, None), (4, "skewed", False, None),
                                                                (3, "zipf", False, None), (3, "uniform", True, 1000),
-                                                               (2, "skewed", False, 777)])
+                                                               (2, "skewed", False, 777), (8, "uniform", True, 3000),
+                                                               (8, "zipf", False, None)])
 def test_dist_sort_gloo(tmp_path, world, dist_name, pairs, max_message):
     """max_message: pieces per message in the exchange (multi.MAX_MESSAGE, 2^27 keys by default,
     works around RCCL dropping the second half of >= 2 GiB messages): small values force rounds."""
