@@ -209,10 +209,11 @@ def main():
     if a.pairs:
         vals = rs.empty_u32(n, dev)
         rs.gen_iota(vals, rank * n)
-    out = rs.empty_u32(n, dev)
-    vout = rs.empty_u32(n, dev) if a.pairs else None
     p = rs.plan(n, a.k, a.pairs, a.tiles_per_chunk)
-    ws = rs.workspace(p.workspace_bytes, dev)
+    # the single-GPU sort's buffers (the multi-GPU step allocates its own)
+    out = rs.empty_u32(n, dev) if not use_dist else None
+    vout = rs.empty_u32(n, dev) if a.pairs and not use_dist else None
+    ws = rs.workspace(p.workspace_bytes, dev) if not use_dist else None
 
     if use_dist:
         import multi
