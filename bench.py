@@ -256,7 +256,7 @@ def main():
     scatter_ms = sc["ms"] / max(1, sc["launches"])
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     achieved = bytes_per_key * keys_per_launch / (scatter_ms * 1e-3) / 1e9
-    kernel = rs.scatter_kernel_name(p) if not use_dist else "rs_scatter"
+    kernel = rs.scatter_kernel_name(p) if not use_dist else "rs_scatter_lines (partition and sort passes)"
     cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel}"
     traffic, traffic_src = traffic_for(cfg_key)
 
