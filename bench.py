@@ -15,6 +15,7 @@ all-reduce, partition, one all-to-all over xGMI, local sort) -> weak scaling.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -32,6 +33,21 @@ import radixsort as rs  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Library banners (gloo's peer count, RCCL's version block) print to fd 1 during setup; keep
+    rank 0's stdout to the one JSON line the driver parses."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,9 +60,15 @@ def parse():
     ap.add_argument("--rank", choices=["match", "split"], default="match")
     ap.add_argument("--tiles-per-chunk", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline sample")
+    ap.add_argument("--cpu-n", type=int, default=1 << 26, help="keys in the CPU-baseline headline sample")
     ap.add_argument("--cpu-reps", type=int, default=3)
-    ap.add_argument("--vendor", action="store_true", help="also time rocPRIM's radix sort")
+    ap.add_argument("--cpu-rows", default="20,30",
+                    help="log2 sizes of extra Baseline1 rows (C1 = 2^20 and the GPU size), '' for none")
+    ap.add_argument("--no-vendor", action="store_true", help="skip the rocPRIM radix sort column")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the reference-style host->host time (H2D + sort + D2H, Parallel7.cu:646-661)")
+    ap.add_argument("--dist-impl", choices=["c", "torch"], default="c",
+                    help="multi-GPU step: rsort_u32_multi over RCCL (c) or multi.py over torch.distributed")
     ap.add_argument("--dist-path", action="store_true",
                     help="run the multi-GPU sort (partition, RCCL all-to-all, local sort) even on one "
                          "rank: its overhead against the single-GPU sort")
@@ -57,8 +79,11 @@ def parse():
     return ap.parse_args()
 
 
-def traffic_for(config_key: str):
-    """HBM bytes per scatter launch from the committed PMC profile (profiles/*pmc*.json), or None."""
+def profile_record(config_key: str):
+    """The newest committed profile record of this configuration (profiles/*pmc*.json, newest
+    round last): HBM bytes per scatter launch from the PMC passes and the rocprofv3 --stats
+    average duration of the same kernel; (record, file name) or (None, None)."""
+    best = (None, None)
     for f in sorted((ROOT / "profiles").glob("*pmc*.json")):
         try:
             d = json.loads(f.read_text())
@@ -66,43 +91,76 @@ def traffic_for(config_key: str):
             continue
         rec = d.get("configs", {}).get(config_key)
         if rec and rec.get("hbm_bytes_per_launch"):
-            return rec["hbm_bytes_per_launch"], f.name
-    return None, None
+            best = (rec, f.name)
+    return best
 
 
-def cpu_baseline(n, k, reps, dist):
-    """Baseline1's sortByHost on this host, single thread: the reference's own code from
-    oracle/_ref when it was built (kind "reference"), else the oracle port (kind "port")."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import _util  # test/bench infrastructure: the oracle loaders (never the product path)
-    x = _util.uniform_keys(n) if dist == "uniform" else _util.zipf_keys(n)
-    out = np.empty_like(x)
-    ref = _util.ref_lib()
-    if ref is not None:
-        kind = "reference"
-        fn = lambda: ref.ref_sort_by_host(_util._ptr(x), n, _util._ptr(out), k)  # noqa: E731
-    else:
-        kind = "port"
-        fn = lambda: _util.oracle().oracle_sort_by_host(_util._ptr(x), n, _util._ptr(out), k)  # noqa: E731
-    times = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        fn()
-        times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    model = ""
+def _pin_one_core():
+    """Pin this process to one CPU it may run on (os.sched_setaffinity, no re-exec); returns the
+    previous set so the caller can restore it."""
+    try:
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {min(old)})
+        return old
+    except (AttributeError, OSError):
+        return None
+
+
+def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
+    return "host CPU"
+
+
+def cpu_baseline(host_keys, n, k, reps, dist, rows):
+    """Baseline1's sortByHost on this host, ONE thread pinned to one core: the reference's own code
+    from oracle/_ref when it was built (kind "reference"), else the oracle port (kind "port").
+    The headline value is the n-key sample (a prefix of the bench's own input, copied from HBM);
+    `rows` adds more sizes (C1 = 2^20 and the GPU size), one run each above 2^26 keys."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _util  # test/bench infrastructure: the oracle loaders (never the product path)
+    ref = _util.ref_lib()
+    kind = "reference" if ref is not None else "port"
+
+    def run(x, out):
+        if ref is not None:
+            ref.ref_sort_by_host(_util._ptr(x), x.size, _util._ptr(out), k)
+        else:
+            _util.oracle().oracle_sort_by_host(_util._ptr(x), x.size, _util._ptr(out), k)
+
+    old = _pin_one_core()
+    try:
+        def timed(m, nreps):
+            x = np.ascontiguousarray(host_keys[:m])
+            out = np.empty_like(x)
+            ts = []
+            for _ in range(nreps):
+                t0 = time.perf_counter()
+                run(x, out)
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts))
+
+        med = timed(n, reps)
+        extra = {}
+        for lg in rows:
+            m = 1 << lg
+            if m > host_keys.size:
+                continue
+            t = timed(m, reps if m <= (1 << 26) else 1)
+            extra[f"2^{lg}"] = {"keys": m, "Mkeys_per_s": round(m / t / 1e6, 2), "ms_per_sort": round(t * 1e3, 2),
+                                "runs": reps if m <= (1 << 26) else 1}
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
     return {"value": round(n / med / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": kind,
-            "sample": f"{n} {dist} u32 keys, k={k}, median of {reps} single-thread runs "
-                      f"({med * 1e3:.0f} ms each) of Baseline1 sortByHost on {model or 'host CPU'} "
-                      f"(host has {os.cpu_count()} logical CPUs)",
-            "ms_per_sort": round(med * 1e3, 2)}
+            "sample": f"{n} {dist} u32 keys (a prefix of the bench input), k={k}, median of {reps} runs "
+                      f"({med * 1e3:.0f} ms each) of Baseline1 sortByHost, one thread pinned to one core of "
+                      f"{_cpu_model()} (host has {os.cpu_count()} logical CPUs)",
+            "ms_per_sort": round(med * 1e3, 2), "rows": extra}
 
 
 def primitives(a, dev):
@@ -171,13 +229,15 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
     # RSORT_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on fewer GPUs
-    # (host-side exchange; timings meaningless). The driver's runs use RCCL, one rank per GPU.
-    backend = os.environ.get("RSORT_BENCH_BACKEND", "nccl")
-    if backend == "gloo":
+    # (multi.py with a host-side exchange; timings meaningless). The driver's runs use RCCL.
+    rehearsal = os.environ.get("RSORT_BENCH_BACKEND", "") == "gloo"
+    if rehearsal:
         local = local % max(1, torch.cuda.device_count())
+        a.dist_impl = "torch"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or a.dist_path
+    dist = None
     if use_dist:
         import torch.distributed as dist
         if world == 1:
@@ -185,10 +245,13 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29517")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        # control plane (barriers, the time max, the RCCL id) on gloo; the keys move over RCCL:
+        # rsort_u32_multi's own communicator (c) or torch's nccl process group (torch)
+        with stdout_to_stderr():
+            if a.dist_impl == "torch" and not rehearsal:
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
     rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
     rs.set_group_chunks(not a.no_group_chunks)
     if a.primitives:
@@ -209,29 +272,46 @@ def main():
     if a.pairs:
         vals = rs.empty_u32(n, dev)
         rs.gen_iota(vals, rank * n)
+    fp_in = rs.fingerprint(keys, vals)[0]
     p = rs.plan(n, a.k, a.pairs, a.tiles_per_chunk)
-    # the single-GPU sort's buffers (the multi-GPU step allocates its own)
-    out = rs.empty_u32(n, dev) if not use_dist else None
-    vout = rs.empty_u32(n, dev) if a.pairs and not use_dist else None
-    ws = rs.workspace(p.workspace_bytes, dev) if not use_dist else None
 
-    if use_dist:
-        import multi
-        ops = multi.GpuOps(dev)
+    comm = None
+    if use_dist and a.dist_impl == "c":
+        uid = [rs.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        with stdout_to_stderr():
+            comm = rs.RcclComm(world, rank, uid[0])
+        cap = rs.default_capacity(n)
+        out = rs.empty_u32(cap, dev)
+        vout = rs.empty_u32(cap, dev) if a.pairs else None
+        ws = rs.workspace(int(rs._lib().rsort_multi_workspace_size(n, cap, a.k, int(a.pairs), world)), dev)
+        res = {}
 
         def step():
-            return multi.dist_sort(keys, a.k, vals=vals, ops=ops)
+            res["out"] = rs.multi_sort_device(comm, keys, a.k, vals=vals, capacity=cap, ws=ws, out=(out, vout))
+    elif use_dist:
+        import multi
+        ops = multi.GpuOps(dev)
+        res = {}
+
+        def step():
+            res["out"] = multi.dist_sort(keys, a.k, vals=vals, ops=ops)
     else:
+        out = rs.empty_u32(n, dev)
+        vout = rs.empty_u32(n, dev) if a.pairs else None
+        ws = rs.workspace(p.workspace_bytes, dev)
+
         def step():
             rs.sort_device(keys, out, a.k, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
+    with stdout_to_stderr():  # torch's nccl group connects on its first collective
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
-            torch.distributed.barrier()
+            dist.barrier()
 
     barrier()
     torch.cuda.synchronize()
@@ -242,11 +322,39 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     barrier()
-    groups = rs.group_flags(p, ws) if not use_dist else None
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    el = torch.tensor([t1 - t0], dtype=torch.float64)
     if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+
+    # the timed output, checked on the device: sorted, same (key, value) multiset as the input
+    # (summed over ranks for the multi-GPU step: each rank's slice is sorted, and the slices are
+    # in order across ranks -- rank r's last key <= rank r + 1's first)
+    if use_dist:
+        ok, ov, _ = res["out"]
+        fp_out, desc = rs.fingerprint(ok, ov)
+
+        def s64(x):  # u64 fingerprint as an int64 tensor element
+            return x - (1 << 64) if x >= (1 << 63) else x
+        first = int(ok[0].item()) & 0xFFFFFFFF if ok.numel() else -1
+        last = int(ok[-1].item()) & 0xFFFFFFFF if ok.numel() else -1
+        mine = torch.tensor([s64(fp_in), s64(fp_out), desc, ok.numel(), first, last], dtype=torch.int64)
+        parts = [torch.zeros(6, dtype=torch.int64) for _ in range(world)]
+        if world > 1:
+            dist.all_gather(parts, mine)
+        else:
+            parts = [mine]
+        parts = [[int(v) for v in x] for x in parts]
+        fin = sum(x[0] for x in parts) & 0xFFFFFFFFFFFFFFFF
+        fout = sum(x[1] for x in parts) & 0xFFFFFFFFFFFFFFFF
+        nonempty = [x for x in parts if x[3] > 0]
+        ordered = all(nonempty[i][5] <= nonempty[i + 1][4] for i in range(len(nonempty) - 1))
+        verified = (fin == fout and sum(x[2] for x in parts) == 0 and ordered
+                    and sum(x[3] for x in parts) == n * world)
+    else:
+        fp_out, desc = rs.fingerprint(out, vout)
+        verified = fp_out == fp_in and desc == 0
+    groups = rs.group_flags(p, ws) if not use_dist else None
 
     # per-kernel: the fused local-sort + scatter pass (the dominant kernel)
     sc = prof.times["scatter"]
@@ -255,13 +363,14 @@ def main():
     bytes_per_key = 16 if a.pairs else 8
     scatter_ms = sc["ms"] / max(1, sc["launches"])
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
-    achieved = bytes_per_key * keys_per_launch / (scatter_ms * 1e-3) / 1e9
+    algo_bytes = bytes_per_key * keys_per_launch
+    achieved = algo_bytes / (scatter_ms * 1e-3) / 1e9
     kernel = rs.scatter_kernel_name(p) if not use_dist else "rs_scatter_lines (partition and sort passes)"
     cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel}"
-    traffic, traffic_src = traffic_for(cfg_key)
+    prec, prec_src = profile_record(cfg_key) if not use_dist else (None, None)
 
     vendor = None
-    if a.vendor and world == 1:
+    if not a.no_vendor and not use_dist and not a.pairs:
         vo = rs.empty_u32(n, dev)
         vws = rs.workspace(int(rs._lib().rsort_vendor_workspace_size(n)), dev)
         rs.vendor_sort_device(keys, vo, ws=vws)
@@ -272,11 +381,41 @@ def main():
         torch.cuda.synchronize()
         tv = (time.perf_counter() - tv) / a.steps
         vendor = {"value": round(n / tv / 1e6, 1), "unit": "Mkeys/s", "ms_per_sort": round(tv * 1e3, 3),
-                  "impl": "rocprim::radix_sort_keys"}
+                  "impl": "rocprim::radix_sort_keys (what sortByThrust resolves to on ROCm, Parallel7.cu:69-73)",
+                  "ours_over_vendor": round((n / (elapsed / a.steps)) / (n / tv), 2)}
         del vo, vws
+
+    host_keys = None
+    e2e = None
+    if rank == 0 and not use_dist and ((not a.no_cpu) or not a.no_e2e):
+        host_keys = rs.to_numpy_u32(keys)
+    if host_keys is not None and not a.no_e2e and not a.pairs:
+        # the reference's timing of sort(..., SORT_BY_DEVICE): device malloc + H2D + sort + D2H of
+        # pageable host buffers (Parallel7.cu:646-661), through rsort_u32_ex; PCIe-bound, not `value`
+        hout = np.empty_like(host_keys)
+        rs.sortByDevice(host_keys, n, hout, a.k)  # first call sizes the library's cached workspace
+        te = time.perf_counter()
+        rs.sortByDevice(host_keys, n, hout, a.k)
+        te = time.perf_counter() - te
+        e2e = {"ms_per_sort": round(te * 1e3, 2), "Mkeys_per_s": round(n / te / 1e6, 1),
+               "what": "host->host sortByDevice (H2D + sort + D2H, pageable buffers, Parallel7.cu:646-661)"}
+        del hout
 
     if rank == 0:
         total_keys = n * world * a.steps
+        roof = {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": prec["hbm_bytes_per_launch"] if prec else None,
+                "traffic_source": prec_src,
+                "algorithmic_bytes_per_launch": int(algo_bytes),
+                "avg_launch_ms": round(scatter_ms, 4),
+                "avg_launch_source": "HIP events around every scatter launch of the timed steps"}
+        if prec and prec.get("rocprof_avg_ns"):
+            rp = prec["rocprof_avg_ns"] * 1e-6
+            roof["avg_launch_ms_rocprof"] = round(rp, 4)
+            roof["frac_rocprof"] = round(algo_bytes / (rp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            roof["rocprof_source"] = prec.get("rocprof_source")
         line = {
             "metric": "Mkeys/s sorting 2^30 uniform uint32; scatter-pass achieved HBM GB/s",
             "value": round(total_keys / elapsed / 1e6, 1),
@@ -298,23 +437,25 @@ def main():
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
                        "group_chunk_passes": ([2 * i + 1 for i, f in enumerate(groups) if f]
                                               if groups is not None else None),
-                       "parallelism": "single GPU" if not use_dist else f"range-partition x{world} (RCCL all-to-all)"},
-            "roofline": {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": int(bytes_per_key * keys_per_launch),
-                         "avg_launch_ms": round(scatter_ms, 4)},
+                       "parallelism": "single GPU" if not use_dist else
+                       f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'})"},
+            "verified": bool(verified),
+            "roofline": roof,
             "phases_ms_per_step": {"histogram": round(hi["ms"] / a.steps, 4), "scan": round(scan["ms"] / a.steps, 4),
                                    "scatter": round(sc["ms"] / a.steps, 4)},
         }
         if vendor:
             line["vendor"] = vendor
-        if not use_dist and not a.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(min(a.cpu_n, n), a.k, a.cpu_reps, a.dist)
+        if e2e:
+            line["end_to_end"] = e2e
+        if host_keys is not None and not a.no_cpu:
+            rows = [int(x) for x in a.cpu_rows.split(",") if x.strip()]
+            line["cpu_baseline"] = cpu_baseline(host_keys, min(a.cpu_n, n), a.k, a.cpu_reps, a.dist, rows)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if use_dist:
-        torch.distributed.destroy_process_group()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -717,6 +717,22 @@ int rsort_top_histogram_sampled(const uint32_t *d_keys, int64_t n, int top_bits,
     return hip_status(launch_top_hist_sampled(d_keys, (uint64_t)n, (uint32_t)top_bits, (uint32_t)stride, d_hist, s));
 }
 
+int rsort_sample_device(const uint32_t *d_keys, int64_t n, int64_t stride, int64_t count, int64_t row_len,
+                        uint32_t *d_out, void *stream) {
+    if (n < 0 || n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (stride < 1 || count < 0 || row_len < count || (row_len > 0 && !d_out) || (count > 0 && n > 0 && !d_keys))
+        return RSORT_ERR_ARG;
+    return hip_status(launch_sample(d_keys, (uint64_t)n, (uint64_t)stride, (uint64_t)count, (uint64_t)row_len, d_out,
+                                    (hipStream_t)stream));
+}
+
+int rsort_fingerprint_device(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint64_t *d_out,
+                             void *stream) {
+    if (n < 0 || n >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (!d_out || (n > 0 && !d_keys)) return RSORT_ERR_ARG;
+    return hip_status(launch_fingerprint(d_keys, d_vals, (uint64_t)n, (unsigned long long *)d_out, (hipStream_t)stream));
+}
+
 int rsort_gen_uniform(uint32_t *d_out, int64_t n, uint64_t seed, void *stream) {
     if (n < 0) return RSORT_ERR_SIZE;
     if (n == 0) return RSORT_OK;

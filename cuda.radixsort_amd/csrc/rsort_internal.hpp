@@ -130,6 +130,10 @@ hipError_t launch_diff_starts(const uint32_t *starts, uint32_t bins, uint32_t *h
                               hipStream_t s);
 hipError_t launch_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t top_bits, uint32_t stride,
                                    uint32_t *hist, hipStream_t s);
+hipError_t launch_sample(const uint32_t *keys, uint64_t n, uint64_t stride, uint64_t count, uint64_t row_len,
+                         uint32_t *out, hipStream_t s);
+hipError_t launch_fingerprint(const uint32_t *keys, const uint32_t *vals, uint64_t n, unsigned long long *out,
+                              hipStream_t s);
 hipError_t launch_gen_uniform(uint32_t *out, uint64_t n, uint64_t seed, hipStream_t s);
 hipError_t launch_gen_zipf(uint32_t *out, uint64_t n, uint64_t seed, const uint32_t *cdf,
                            uint64_t ranks, hipStream_t s);

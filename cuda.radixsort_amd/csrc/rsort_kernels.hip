@@ -1392,6 +1392,17 @@ __global__ __launch_bounds__(1024) void rs_top_hist_sampled(const uint32_t *keys
         if (s_h[i]) atomicAdd(&hist[i], s_h[i]);
 }
 
+// The multi-GPU sort's splitter sample (rsort_multi_sample_plan): out[j] = keys[min(n - 1, j * stride +
+// stride / 2)] for j < count, padded with 0xFFFFFFFF up to row_len (the padding sorts last).
+__global__ void rs_sample(const uint32_t *keys, uint64_t n, uint64_t stride, uint64_t count, uint64_t row_len,
+                          uint32_t *out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < row_len; j += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t v = 0xFFFFFFFFu;
+        if (j < count && n > 0) v = keys[min(n - 1, j * stride + stride / 2)];
+        out[j] = v;
+    }
+}
+
 __global__ void rs_gather_starts(const uint32_t *table, uint32_t num_chunks, uint32_t bins,
                                  uint64_t n, uint32_t *starts) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1423,6 +1434,39 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
     h *= 0xC2B2AE35u;
     h ^= h >> 16;
     return h;
+}
+
+// Order-independent fingerprint of a key (or key + value) multiset and the count of adjacent
+// descents: out[0] += sum of fmix64(value << 32 | key), out[1] += #{i : keys[i] > keys[i + 1]}.
+// A sorted permutation of the input has the input's out[0] and out[1] == 0 (bench.py's check
+// of the timed output; rsort_fingerprint_device).
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 33;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void rs_fingerprint(const uint32_t *keys, const uint32_t *vals, uint64_t n,
+                                                      unsigned long long *out) {
+    uint64_t h = 0, desc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = keys[i];
+        const uint64_t v = vals ? vals[i] : 0u;
+        h += fmix64((v << 32) | k);
+        if (i + 1 < n && k > keys[i + 1]) ++desc;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        h += (uint64_t)__shfl_xor((unsigned long long)h, o);
+        desc += (uint64_t)__shfl_xor((unsigned long long)desc, o);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(&out[0], (unsigned long long)h);
+        if (desc) atomicAdd(&out[1], (unsigned long long)desc);
+    }
 }
 
 __global__ void rs_gen_uniform(uint32_t *out, uint64_t n, uint64_t seed) {
@@ -1729,6 +1773,22 @@ hipError_t launch_top_hist_sampled(const uint32_t *keys, uint64_t n, uint32_t to
     const uint64_t blocks = ((n + 255) / 256 + stride - 1) / stride;  // sampled blocks
     const unsigned grid = (unsigned)std::min<uint64_t>(std::max<uint64_t>(blocks / 16, 1), 256);
     rs_top_hist_sampled<<<grid, 1024, 0, s>>>(keys, n, top_bits, stride, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample(const uint32_t *keys, uint64_t n, uint64_t stride, uint64_t count, uint64_t row_len,
+                         uint32_t *out, hipStream_t s) {
+    if (row_len == 0) return hipSuccess;
+    rs_sample<<<(unsigned)std::min<uint64_t>((row_len + 255) / 256, 4096), 256, 0, s>>>(keys, n, stride, count,
+                                                                                        row_len, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fingerprint(const uint32_t *keys, const uint32_t *vals, uint64_t n, unsigned long long *out,
+                              hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, 16, s);
+    if (e != hipSuccess || n == 0) return e;
+    rs_fingerprint<<<(unsigned)std::min<uint64_t>((n + 255) / 256, 8192), 256, 0, s>>>(keys, vals, n, out);
     return hipGetLastError();
 }
 

@@ -1,15 +1,30 @@
-// rsort_multi.cpp -- rsort_u32_multi: the multi-GPU sort over an RCCL communicator (C ABI).
+// rsort_multi.cpp -- the multi-GPU sort (C ABI): rsort_u32_multi over an RCCL communicator and
+// rsort_u32_multi_transport over any rsort_transport (the in-process loopback below is one).
 //
 // No reference counterpart (the reference sorts on one GPU, Parallel7.cu:10/:697); this is
-// SURVEY.md §8e / BASELINE config 5, the same algorithm as cuda.radixsort_amd/multi.py (which
-// drives it through torch.distributed): top-bits histogram, one all-reduce, splitters on bin
-// edges, a stable partition into `world` key ranges, the count matrix by all-gather, ONE
-// exchange (grouped send/recv: each pair of GPUs talks over its own xGMI link), a local sort.
+// SURVEY.md §8e / BASELINE config 5, the same protocol as cuda.radixsort_amd/multi.py (which
+// drives the same pure planning functions through torch.distributed):
+//   1. all-gather every rank's key count; the sampling plan (rsort_multi_sample_plan)
+//   2. a regular sample of the local keys, all-gathered, sorted on the device: the world - 1
+//      global quantile keys (exact key values, not bin edges)
+//   3. splitters with an equal-keys bucket per quantile key (rsort_multi_splitters_make), a
+//      stable partition of the local keys into those buckets
+//   4. all-gather of the bucket counts and capacities; the exchange plan (rsort_multi_exchange_plan)
+//      -- identical on every rank, so a capacity error is returned by all ranks together before
+//      any key moves
+//   5. ONE exchange: the rank's own range by a device copy, every other message point to point
+//      (each pair of GPUs on its own xGMI link), cut into equal rounds of <= 2^28 keys
+//   6. local LSD sort of what arrived, in place.
+#include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <vector>
 
 #include "rsort.h"
@@ -19,25 +34,34 @@ using namespace rsort;
 
 namespace {
 
-constexpr int kTopBits = 12;
-// splitters come from every 16th block of 256 keys: their balance only sets the load per rank
-constexpr int kSampleStride = 16;
-constexpr int kMaxRanks = kMaxSplitters + 1;
-// keys per RCCL message piece (512 MiB): 1 GiB messages arrive whole, 2 GiB ones do not
-constexpr unsigned long long kMaxMessage = 1ull << 27;
+constexpr int kMaxRanks = RSORT_MAX_RANKS;
+constexpr int kMaxBuckets = 2 * kMaxRanks;
+// total sample budget over all ranks: quantile error ~ sqrt(1/4/2^20) of the keys (0.05 %)
+constexpr int64_t kSampleBudget = (int64_t)1 << 20;
+// keys per message of one exchange round (1 GiB): this RCCL (2.26, ROCm 7) leaves the second half
+// of an all_to_all / send message of >= 2 GiB unwritten without an error (dev/a2a_lab.py); 1 GiB
+// messages arrive whole
+constexpr int64_t kMaxPiece = (int64_t)1 << 28;
+std::atomic<int64_t> g_piece{kMaxPiece};  // rsort_set_exchange_piece (tests force several rounds)
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct MultiCarve {
-    uint32_t *part_k, *part_v, *hist32, *starts;
-    unsigned long long *hist64, *sendc, *allc;
-    void *sub;  // shared by the top histogram, the partition and the local sort (used in turn)
+    uint32_t *part_k, *part_v;
+    uint64_t *n_send, *n_all;      // [2], [world][2]: key count, values flags
+    uint64_t *c_send, *c_all;      // [kMaxBuckets + 1], [world][kMaxBuckets + 1]
+    uint32_t *starts;              // [kMaxBuckets + 1]
+    uint32_t *samp_send, *samp_all;  // [kSampleBudget], [world][kSampleBudget]
+    void *sub;                     // partition, sample sort and local sort, in turn
     size_t sub_bytes;
 };
 
+int64_t samples_per_rank(int world) { return std::max<int64_t>(1, kSampleBudget / world); }
+
 size_t sub_bytes(int64_t n, int64_t cap, int k, int pairs, int world) {
-    size_t a = rsort_workspace_size(n, kTopBits, 0);
-    size_t b = rsort_partition_workspace_size(n, world, pairs);
+    size_t a = rsort_partition_workspace_size(n, std::min(2 * world - 1, kMaxSplitters + 1), pairs);
+    // the gathered sample: world rows of at most kSampleBudget samples
+    size_t b = rsort_workspace_size(world * kSampleBudget, 8, 0) + ((size_t)4 << 8 << 12);
     // the received count is only known later; a smaller n can pick a geometry with a larger
     // chunk table (<= 2^k x 4096 entries), so leave room for that
     size_t c = rsort_workspace_size(std::max<int64_t>(cap, 1), k, pairs) + ((size_t)4 << k << 12);
@@ -54,38 +78,275 @@ size_t multi_bytes(int64_t n, int64_t cap, int k, int pairs, int world, MultiCar
     MultiCarve m{};
     m.part_k = (uint32_t *)take((size_t)n * 4);
     m.part_v = pairs ? (uint32_t *)take((size_t)n * 4) : nullptr;
-    m.hist32 = (uint32_t *)take((size_t)(1 << kTopBits) * 4);
-    m.hist64 = (unsigned long long *)take((size_t)(1 << kTopBits) * 8);
-    m.starts = (uint32_t *)take((size_t)(kMaxRanks + 1) * 4);
-    m.sendc = (unsigned long long *)take((size_t)kMaxRanks * 8);
-    m.allc = (unsigned long long *)take((size_t)kMaxRanks * kMaxRanks * 8);
+    m.n_send = (uint64_t *)take(16);
+    m.n_all = (uint64_t *)take((size_t)kMaxRanks * 16);
+    m.c_send = (uint64_t *)take((size_t)(kMaxBuckets + 1) * 8);
+    m.c_all = (uint64_t *)take((size_t)kMaxRanks * (kMaxBuckets + 1) * 8);
+    m.starts = (uint32_t *)take((size_t)(kMaxBuckets + 1) * 4);
+    m.samp_send = (uint32_t *)take((size_t)kSampleBudget * 4);
+    m.samp_all = (uint32_t *)take((size_t)world * kSampleBudget * 4);
     m.sub_bytes = sub_bytes(n, cap, k, pairs, world);
     m.sub = take(m.sub_bytes);
     if (mc) *mc = m;
     return off;
 }
 
-// world-1 ascending splitters on bin edges of the global top-bits histogram: bucket i ends with
-// the first bin whose inclusive prefix reaches (i+1)*total/world (multi.py:choose_splitters).
-std::vector<uint32_t> choose_splitters(const std::vector<unsigned long long> &hist, int world) {
-    std::vector<unsigned long long> cum(hist.size());
-    unsigned long long acc = 0;
-    for (size_t i = 0; i < hist.size(); ++i) cum[i] = (acc += hist[i]);
-    const unsigned long long total = acc;
-    const int shift = 32 - kTopBits;
-    std::vector<uint32_t> out;
-    for (int i = 1; i < world; ++i) {
-        const unsigned long long target = (total * (unsigned long long)i) / (unsigned long long)world;
-        const size_t b = (size_t)(std::lower_bound(cum.begin(), cum.end(), target) - cum.begin());
-        const size_t edge = b + 1;
-        uint32_t sp = edge < hist.size() ? (uint32_t)(edge << shift) : 0xFFFFFFFFu;
-        if (!out.empty()) sp = std::max(sp, out.back());
-        out.push_back(sp);
-    }
-    return out;
+int hip_st(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP; }
+
+// ------------------------------------------------------------------------------ RCCL transport
+struct RcclCtx {
+    ncclComm_t comm;
+};
+
+int rccl_allgather(void *ctx, const void *d_send, void *d_recv, size_t bytes, void *stream) {
+    ncclComm_t comm = static_cast<RcclCtx *>(ctx)->comm;
+    return ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, (hipStream_t)stream) == ncclSuccess ? RSORT_OK
+                                                                                                     : RSORT_ERR_COMM;
 }
 
-int nccl_status(ncclResult_t r) { return r == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM; }
+int rccl_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void *const *d_recv,
+                  const size_t *recv_bytes, void *stream) {
+    ncclComm_t comm = static_cast<RcclCtx *>(ctx)->comm;
+    int world = 0, me = 0;
+    if (ncclCommCount(comm, &world) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess) return RSORT_ERR_COMM;
+    hipStream_t s = (hipStream_t)stream;
+    // every call inside the group is checked; the group is always closed (an open group would
+    // leave the communicator unusable), and the first failure is returned
+    ncclResult_t first = ncclGroupStart();
+    if (first != ncclSuccess) return RSORT_ERR_COMM;
+    for (int p = 0; p < world; ++p) {
+        if (p == me) continue;
+        if (send_bytes[p]) {
+            const ncclResult_t r = ncclSend(d_send[p], send_bytes[p], ncclUint8, p, comm, s);
+            if (first == ncclSuccess) first = r;
+        }
+        if (recv_bytes[p]) {
+            const ncclResult_t r = ncclRecv(d_recv[p], recv_bytes[p], ncclUint8, p, comm, s);
+            if (first == ncclSuccess) first = r;
+        }
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    if (first == ncclSuccess) first = e;
+    return first == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM;
+}
+
+// ------------------------------------------------------------------------------ loopback transport
+// World of `world` ranks in one process (one thread per rank, any devices with peer access, or one
+// device): collectives through a host rendezvous and device-to-device copies. Test transport for
+// the multi-GPU path on a one-GPU box (RCCL refuses two ranks on one device: "Duplicate GPU
+// detected"); every wait is bounded so a protocol bug ends in RSORT_ERR_COMM, not a hang.
+struct LoopbackGroup;
+struct LoopbackCtx {
+    LoopbackGroup *g;
+    int rank;
+};
+
+struct LoopbackGroup {
+    int world;
+    LoopbackCtx ctx[kMaxRanks];
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    bool broken = false;
+    // posted by each rank between two barriers
+    const void *ag_src[kMaxRanks];
+    size_t ag_bytes[kMaxRanks];
+    void *const *ex_send[kMaxRanks];
+    const size_t *ex_send_bytes[kMaxRanks];
+
+    // returns false on timeout (and marks the group broken so every rank fails fast)
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const uint64_t gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen || broken; });
+        if (!ok || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
+int lb_allgather(void *ctx, const void *d_send, void *d_recv, size_t bytes, void *stream) {
+    LoopbackCtx *c = static_cast<LoopbackCtx *>(ctx);
+    LoopbackGroup *g = c->g;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;  // d_send is ready
+    g->ag_src[c->rank] = d_send;
+    g->ag_bytes[c->rank] = bytes;
+    if (!g->barrier()) return RSORT_ERR_COMM;
+    int st = RSORT_OK;
+    for (int r = 0; r < g->world && !st; ++r) {
+        if (g->ag_bytes[r] != bytes) st = RSORT_ERR_COMM;
+        else if (bytes && hipMemcpyAsync((char *)d_recv + (size_t)r * bytes, g->ag_src[r], bytes,
+                                         hipMemcpyDeviceToDevice, s) != hipSuccess)
+            st = RSORT_ERR_HIP;
+    }
+    if (!st && hipStreamSynchronize(s) != hipSuccess) st = RSORT_ERR_HIP;
+    if (!g->barrier()) return RSORT_ERR_COMM;  // nobody reuses its send buffer before all have copied
+    return st;
+}
+
+int lb_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void *const *d_recv,
+                const size_t *recv_bytes, void *stream) {
+    LoopbackCtx *c = static_cast<LoopbackCtx *>(ctx);
+    LoopbackGroup *g = c->g;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    g->ex_send[c->rank] = d_send;
+    g->ex_send_bytes[c->rank] = send_bytes;
+    if (!g->barrier()) return RSORT_ERR_COMM;
+    int st = RSORT_OK;
+    for (int p = 0; p < g->world && !st; ++p) {
+        if (p == c->rank) continue;
+        // what p sends to me must be what I expect to receive from p
+        if (g->ex_send_bytes[p][c->rank] != recv_bytes[p]) st = RSORT_ERR_COMM;
+        else if (recv_bytes[p] && hipMemcpyAsync(d_recv[p], g->ex_send[p][c->rank], recv_bytes[p],
+                                                 hipMemcpyDeviceToDevice, s) != hipSuccess)
+            st = RSORT_ERR_HIP;
+    }
+    if (!st && hipStreamSynchronize(s) != hipSuccess) st = RSORT_ERR_HIP;
+    if (!g->barrier()) return RSORT_ERR_COMM;
+    return st;
+}
+
+// ------------------------------------------------------------------------------ the sort
+int d2h(void *h, const void *d, size_t bytes, hipStream_t s) {
+    if (hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return RSORT_ERR_HIP;
+    return hip_st(hipStreamSynchronize(s));
+}
+
+int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32_t *d_keys_out, uint32_t *d_vals_out,
+               int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits, const rsort_transport *tr,
+               void *d_workspace, size_t workspace_bytes, hipStream_t s) {
+    if (k_bits < kMinBits || k_bits > kMaxBits) return RSORT_ERR_BITS;
+    if (n < 0 || n >= ((int64_t)1 << 32) || capacity < 0 || capacity >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
+    if (!tr || !tr->allgather || !tr->exchange || !out_n || !out_offset || !d_workspace) return RSORT_ERR_ARG;
+    // a rank sorts pairs when it passes values or a values output (a rank with no keys may pass
+    // an empty, NULL values input); the ranks agree on it in step 1
+    const int pairs = (d_vals != nullptr || d_vals_out != nullptr) ? 1 : 0;
+    if ((n > 0 && !d_keys) || (capacity > 0 && !d_keys_out)) return RSORT_ERR_ARG;
+    const int world = tr->world, me = tr->rank;
+    if (world < 1 || world > kMaxRanks || me < 0 || me >= world) return RSORT_ERR_ARG;
+    MultiCarve m;
+    if (workspace_bytes < multi_bytes(n, capacity, k_bits, pairs, world, &m, d_workspace)) return RSORT_ERR_WORKSPACE;
+    int st;
+
+    // 1. key counts and value flags -> sampling plan; a values mismatch between ranks is an
+    //    argument error on every rank (all see the same flags)
+    const uint64_t mine[2] = {(uint64_t)n, (uint64_t)(pairs | (d_vals ? 2 : 0) | (d_vals_out ? 4 : 0))};
+    if (hipMemcpyAsync(m.n_send, mine, 16, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
+    if ((st = tr->allgather(tr->ctx, m.n_send, m.n_all, 16, s))) return st;
+    uint64_t nf[2 * kMaxRanks];
+    if ((st = d2h(nf, m.n_all, (size_t)world * 16, s))) return st;
+    int64_t n_all[kMaxRanks];
+    bool any_pairs = false, bad = false;
+    for (int r = 0; r < world; ++r) {
+        n_all[r] = (int64_t)nf[2 * r];
+        any_pairs |= (nf[2 * r + 1] & 1) != 0;
+    }
+    for (int r = 0; r < world && any_pairs; ++r)
+        bad |= !(nf[2 * r + 1] & 4) || (n_all[r] > 0 && !(nf[2 * r + 1] & 2));
+    if (bad) return RSORT_ERR_ARG;
+    rsort_sample_plan sp;
+    if ((st = rsort_multi_sample_plan(world, n_all, samples_per_rank(world), &sp))) return st;
+
+    // 2. sample, gather, sort on the device, read the quantile keys
+    if (sp.row_len > kSampleBudget) return RSORT_ERR_ARG;  // cannot happen: budget / world per rank
+    if (launch_sample(d_keys, (uint64_t)n, (uint64_t)sp.stride, (uint64_t)sp.count[me], (uint64_t)sp.row_len,
+                      m.samp_send, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if ((st = tr->allgather(tr->ctx, m.samp_send, m.samp_all, (size_t)sp.row_len * 4, s))) return st;
+    uint32_t q[kMaxRanks] = {0};
+    if (world > 1 && sp.total > 0) {
+        const int64_t ns = (int64_t)world * sp.row_len;
+        if ((st = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s))) return st;
+        for (int i = 1; i < world; ++i)
+            if (hipMemcpyAsync(&q[i - 1], m.samp_all + rsort_multi_quantile_index(&sp, i), 4, hipMemcpyDeviceToHost,
+                               s) != hipSuccess)
+                return RSORT_ERR_HIP;
+        if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    }
+    rsort_multi_splitters spl;
+    if ((st = rsort_multi_splitters_make(world, q, &spl))) return st;
+
+    // 3. stable partition into the splitters' buckets
+    const int buckets = spl.nsplit + 1;
+    if (buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;
+    if ((st = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, spl.split, buckets, m.starts, m.sub,
+                                     m.sub_bytes, s)))
+        return st;
+    uint32_t starts[kMaxBuckets + 1];
+    if ((st = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s))) return st;
+
+    // 4. count matrix + capacities -> exchange plan (the same on every rank)
+    uint64_t row[kMaxBuckets + 1];
+    for (int b = 0; b < buckets; ++b) row[b] = (uint64_t)(starts[b + 1] - starts[b]);
+    row[buckets] = (uint64_t)capacity;
+    const size_t row_bytes = (size_t)(buckets + 1) * 8;
+    if (hipMemcpyAsync(m.c_send, row, row_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
+    if ((st = tr->allgather(tr->ctx, m.c_send, m.c_all, row_bytes, s))) return st;
+    uint64_t all[kMaxRanks * (kMaxBuckets + 1)];
+    if ((st = d2h(all, m.c_all, (size_t)world * row_bytes, s))) return st;
+    int64_t counts[kMaxRanks * kMaxBuckets], caps[kMaxRanks];
+    for (int r = 0; r < world; ++r) {
+        for (int b = 0; b < buckets; ++b) counts[r * buckets + b] = (int64_t)all[r * (buckets + 1) + b];
+        caps[r] = (int64_t)all[r * (buckets + 1) + buckets];
+    }
+    rsort_exchange_plan xp;
+    if ((st = rsort_multi_exchange_plan(world, me, buckets, counts, &spl, caps, &xp))) return st;
+
+    // 5. the exchange: own range by a device copy, the rest in equal rounds of <= kMaxPiece keys
+    if (xp.send_cnt[me] != xp.recv_cnt[me]) return RSORT_ERR_ARG;
+    if (xp.send_cnt[me] > 0) {
+        if (hipMemcpyAsync(d_keys_out + xp.recv_off[me], m.part_k + xp.send_off[me], (size_t)xp.send_cnt[me] * 4,
+                           hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+        if (pairs && hipMemcpyAsync(d_vals_out + xp.recv_off[me], m.part_v + xp.send_off[me],
+                                    (size_t)xp.send_cnt[me] * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+    }
+    const int64_t maxp = g_piece.load();
+    const int64_t rounds = xp.max_message > 0 ? (xp.max_message + maxp - 1) / maxp : 0;
+    const int64_t piece = rounds > 0 ? ((xp.max_message + rounds - 1) / rounds + 63) / 64 * 64 : 0;
+    for (int64_t rd = 0; rd < rounds; ++rd) {
+        for (int arr = 0; arr < (pairs ? 2 : 1); ++arr) {
+            uint32_t *src = arr ? m.part_v : m.part_k;
+            uint32_t *dst = arr ? d_vals_out : d_keys_out;
+            void *sp_[kMaxRanks], *rp_[kMaxRanks];
+            size_t sb[kMaxRanks], rb[kMaxRanks];
+            for (int p = 0; p < world; ++p) {
+                const int64_t a0 = std::min(xp.send_cnt[p], rd * piece), a1 = std::min(xp.send_cnt[p], (rd + 1) * piece);
+                const int64_t b0 = std::min(xp.recv_cnt[p], rd * piece), b1 = std::min(xp.recv_cnt[p], (rd + 1) * piece);
+                sp_[p] = src + xp.send_off[p] + a0;
+                rp_[p] = dst + xp.recv_off[p] + b0;
+                sb[p] = p == me ? 0 : (size_t)(a1 - a0) * 4;
+                rb[p] = p == me ? 0 : (size_t)(b1 - b0) * 4;
+            }
+            if ((st = tr->exchange(tr->ctx, sp_, sb, rp_, rb, s))) return st;
+        }
+    }
+
+    // 6. local sort of what arrived, in place
+    if (xp.n_recv > 0) {
+        rsort_plan p;
+        if ((st = rsort_plan_make(xp.n_recv, k_bits, pairs, 0, &p))) return st;
+        if ((st = rsort_sort_planned(&p, d_keys_out, d_vals_out, d_keys_out, d_vals_out, m.sub, m.sub_bytes, s)))
+            return st;
+    }
+    *out_n = xp.n_recv;
+    *out_offset = xp.offset;
+    return RSORT_OK;
+}
 
 }  // namespace
 
@@ -96,99 +357,52 @@ size_t rsort_multi_workspace_size(int64_t n, int64_t capacity, int k_bits, int p
     return multi_bytes(n, capacity, k_bits, pairs ? 1 : 0, world, nullptr, nullptr);
 }
 
+int rsort_u32_multi_transport(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32_t *d_keys_out,
+                              uint32_t *d_vals_out, int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits,
+                              const rsort_transport *transport, void *d_workspace, size_t workspace_bytes,
+                              void *stream) {
+    return multi_sort(d_keys, d_vals, n, d_keys_out, d_vals_out, capacity, out_n, out_offset, k_bits, transport,
+                      d_workspace, workspace_bytes, (hipStream_t)stream);
+}
+
 int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32_t *d_keys_out,
                     uint32_t *d_vals_out, int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits,
                     void *nccl_comm, void *d_workspace, size_t workspace_bytes, void *stream) {
-    if (k_bits < kMinBits || k_bits > kMaxBits) return RSORT_ERR_BITS;
-    if (n < 0 || n >= ((int64_t)1 << 32) || capacity < 0 || capacity >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
-    if (!nccl_comm || !out_n || !out_offset || !d_workspace) return RSORT_ERR_ARG;
-    const int pairs = d_vals != nullptr;
-    if ((n > 0 && !d_keys) || (capacity > 0 && (!d_keys_out || (pairs && !d_vals_out)))) return RSORT_ERR_ARG;
-    ncclComm_t comm = (ncclComm_t)nccl_comm;
+    if (!nccl_comm) return RSORT_ERR_ARG;
+    RcclCtx ctx{(ncclComm_t)nccl_comm};
     int world = 0, me = 0;
-    if (ncclCommCount(comm, &world) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess)
+    if (ncclCommCount(ctx.comm, &world) != ncclSuccess || ncclCommUserRank(ctx.comm, &me) != ncclSuccess)
         return RSORT_ERR_COMM;
-    if (world < 1 || world > kMaxRanks) return RSORT_ERR_ARG;
-    MultiCarve m;
-    if (workspace_bytes < multi_bytes(n, capacity, k_bits, pairs, world, &m, d_workspace)) return RSORT_ERR_WORKSPACE;
-    hipStream_t s = (hipStream_t)stream;
-    int st;
+    rsort_transport tr{&ctx, world, me, rccl_allgather, rccl_exchange};
+    return multi_sort(d_keys, d_vals, n, d_keys_out, d_vals_out, capacity, out_n, out_offset, k_bits, &tr,
+                      d_workspace, workspace_bytes, (hipStream_t)stream);
+}
 
-    // 1-3: global top-bits histogram -> splitters (host)
-    if ((st = rsort_top_histogram_sampled(d_keys, n, kTopBits, kSampleStride, m.hist32, stream))) return st;
-    if (launch_widen(m.hist32, m.hist64, 1u << kTopBits, s) != hipSuccess) return RSORT_ERR_HIP;
-    if ((st = nccl_status(ncclAllReduce(m.hist64, m.hist64, (size_t)1 << kTopBits, ncclUint64, ncclSum, comm, s))))
-        return st;
-    std::vector<unsigned long long> hist((size_t)1 << kTopBits);
-    if (hipMemcpyAsync(hist.data(), m.hist64, hist.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return RSORT_ERR_HIP;
-    const std::vector<uint32_t> split = choose_splitters(hist, world);
+int64_t rsort_set_exchange_piece(int64_t keys) {
+    const int64_t old = g_piece.load();
+    if (keys >= 64 && keys <= kMaxPiece) g_piece.store(keys);
+    return old;
+}
 
-    // 4: stable partition of the local keys into `world` key ranges
-    if ((st = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, split.data(), world, m.starts, m.sub,
-                                     m.sub_bytes, stream)))
-        return st;
-    uint32_t starts[kMaxRanks + 1];
-    if (hipMemcpyAsync(starts, m.starts, (size_t)(world + 1) * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return RSORT_ERR_HIP;
-    unsigned long long send[kMaxRanks];
-    for (int r = 0; r < world; ++r) send[r] = (unsigned long long)(starts[r + 1] - starts[r]);
-
-    // 5: the world x world count matrix (row = source rank)
-    if (hipMemcpyAsync(m.sendc, send, (size_t)world * 8, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
-    if ((st = nccl_status(ncclAllGather(m.sendc, m.allc, (size_t)world, ncclUint64, comm, s)))) return st;
-    unsigned long long all[kMaxRanks * kMaxRanks];
-    if (hipMemcpyAsync(all, m.allc, (size_t)world * world * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return RSORT_ERR_HIP;
-    unsigned long long recv[kMaxRanks], n_recv = 0, offset = 0;
-    for (int r = 0; r < world; ++r) {
-        recv[r] = all[r * world + me];
-        n_recv += recv[r];
-        for (int q = 0; q < me; ++q) offset += all[r * world + q];
-    }
-    if (n_recv > (unsigned long long)capacity) return RSORT_ERR_CAPACITY;
-
-    // 6: the exchange; chunks land in source-rank order (keeps pairs stable). Every message is
-    // cut into pieces of at most kMaxMessage keys: this RCCL (2.26, ROCm 7) silently leaves the
-    // second half of a >= 2 GiB message unwritten (dev/a2a_lab.py), and with 2^30 keys per GPU
-    // two ranks exchange ~2 GiB each way. The piece count comes from the whole count matrix, so
-    // every rank runs the same number of groups.
-    unsigned long long biggest = 0;
-    for (int i = 0; i < world * world; ++i) biggest = std::max(biggest, all[i]);
-    const unsigned long long pieces = std::max(1ull, (biggest + kMaxMessage - 1) / kMaxMessage);
-    for (unsigned long long q = 0; q < pieces; ++q) {
-        if ((st = nccl_status(ncclGroupStart()))) return st;
-        unsigned long long so = 0, ro = 0;
-        for (int r = 0; r < world; ++r) {
-            const unsigned long long a0 = std::min(send[r], q * kMaxMessage), a1 = std::min(send[r], (q + 1) * kMaxMessage);
-            const unsigned long long b0 = std::min(recv[r], q * kMaxMessage), b1 = std::min(recv[r], (q + 1) * kMaxMessage);
-            if (a1 > a0) {
-                ncclSend(m.part_k + so + a0, a1 - a0, ncclUint32, r, comm, s);
-                if (pairs) ncclSend(m.part_v + so + a0, a1 - a0, ncclUint32, r, comm, s);
-            }
-            if (b1 > b0) {
-                ncclRecv(d_keys_out + ro + b0, b1 - b0, ncclUint32, r, comm, s);
-                if (pairs) ncclRecv(d_vals_out + ro + b0, b1 - b0, ncclUint32, r, comm, s);
-            }
-            so += send[r];
-            ro += recv[r];
-        }
-        if ((st = nccl_status(ncclGroupEnd()))) return st;
-    }
-
-    // 7: local sort of what arrived, in place
-    if (n_recv > 0) {
-        rsort_plan p;
-        if ((st = rsort_plan_make((int64_t)n_recv, k_bits, pairs, 0, &p))) return st;
-        if ((st = rsort_sort_planned(&p, d_keys_out, d_vals_out, d_keys_out, d_vals_out, m.sub, m.sub_bytes, stream)))
-            return st;
-    }
-    *out_n = (int64_t)n_recv;
-    *out_offset = (int64_t)offset;
+int rsort_loopback_create(int world, void **group) {
+    if (!group || world < 1 || world > kMaxRanks) return RSORT_ERR_ARG;
+    LoopbackGroup *g = new (std::nothrow) LoopbackGroup();
+    if (!g) return RSORT_ERR_ALLOC;
+    g->world = world;
+    for (int r = 0; r < world; ++r) g->ctx[r] = LoopbackCtx{g, r};
+    *group = g;
     return RSORT_OK;
+}
+
+int rsort_loopback_transport(void *group, int rank, rsort_transport *out) {
+    LoopbackGroup *g = static_cast<LoopbackGroup *>(group);
+    if (!g || !out || rank < 0 || rank >= g->world) return RSORT_ERR_ARG;
+    *out = rsort_transport{&g->ctx[rank], g->world, rank, lb_allgather, lb_exchange};
+    return RSORT_OK;
+}
+
+void rsort_loopback_destroy(void *group) {
+    delete static_cast<LoopbackGroup *>(group);
 }
 
 }  // extern "C"

@@ -1,23 +1,27 @@
-"""Multi-GPU sort: key-range (MSD bucket) partition with ONE exchange, then a local LSD sort.
+"""Multi-GPU sort over torch.distributed: key-range partition with ONE exchange, then a local LSD sort.
 
-No reference counterpart (the reference is single-GPU, Parallel7.cu:10/:697); this is
-BASELINE config 5 / SURVEY §8e. One process per GPU, torch.distributed over RCCL ("nccl"):
+No reference counterpart (the reference is single-GPU, Parallel7.cu:10/:697); this is BASELINE
+config 5 / SURVEY §8e, the same protocol as the C ABI's rsort_u32_multi (rsort_multi.cpp), and it
+takes every host-side decision from the same pure C planning functions (rsort_multi_sample_plan,
+rsort_multi_splitters_make, rsort_multi_exchange_plan), so both paths split and place keys alike:
 
-  1. top-bits histogram of a 1/16 block sample       (HIP: rsort_top_histogram_sampled)
-  2. all_reduce(SUM) of the 2^top_bits counts        (RCCL, 16 KiB)
-  3. splitters on bin edges balancing ~n/world keys per rank (host, 4096 values)
-  4. stable partition of the local keys into world buckets (HIP: rsort_partition_device)
-  5. all_to_all of the per-destination counts        (RCCL, world x i64)
-  6. all_to_all of the keys (and values)             (RCCL over xGMI: one peer per link;
-                                                      messages cut to <= 512 MiB pieces)
-  7. local LSD sort of what arrived                   (HIP: the single-GPU sort)
+  1. all_gather of the key counts                      -> the sampling plan (one stride for all)
+  2. a regular sample of the local keys (HIP), all_gather, sort (HIP) -> world-1 quantile KEYS
+  3. splitters with an equal-keys bucket per quantile key (world <= 8): a run of equal keys --
+     a hot key, duplicate-heavy input -- is split across ranks in (source rank, position) order
+  4. stable partition into those buckets (HIP: rsort_partition_device)
+  5. all_gather of the bucket counts and capacities    -> the exchange plan, the same on every
+     rank (a capacity overflow raises on ALL ranks before any key moves)
+  6. the exchange: own range by a device copy, every other message by all_to_all (RCCL over
+     xGMI: grouped send/recv), in equal rounds of <= 2^28 keys per message
+  7. local LSD sort of what arrived (HIP)
 
 Rank r ends with the keys of global ranks [offset_r, offset_r + count_r); concatenating the
-ranks' outputs in rank order gives exactly Baseline1's sorted array. Received chunks are
-concatenated in source-rank order, so with values the whole sort stays stable.
+ranks' outputs in rank order gives exactly Baseline1's sorted array. Received chunks are placed
+in source-rank order, so with values the whole sort stays stable.
 
-`LocalOps` carries the three per-device steps; GpuOps (the product) calls librsort.so. Tests
-substitute a numpy implementation to exercise the distributed logic on CPU with gloo.
+The per-device steps go through an `ops` object: GpuOps (the product) calls librsort.so; the CPU
+tests substitute a numpy restatement to exercise the distributed logic with gloo.
 """
 from __future__ import annotations
 
@@ -27,14 +31,13 @@ import torch.distributed as dist
 
 import radixsort as rs
 
-# Keys per RCCL message (512 MiB of u32): the RCCL of this image (2.26, ROCm 7; torch 2.10)
-# silently leaves the second half of an all_to_all message of >= 2 GiB unwritten
-# (dev/a2a_lab.py: 1 GiB arrives whole, 2 GiB - 4 B does not), and two ranks holding 2^30 keys
-# each exchange ~2 GiB each way. Larger exchanges go in rounds of pieces this size.
-MAX_MESSAGE = 1 << 27
-# Splitters come from the top-bits histogram of every 16th block of 256 keys (all ranks sample
-# alike, so the global histogram keeps its proportions; a 2^30-key rank reads 256 MiB, not 4 GiB).
-SAMPLE_STRIDE = 16
+# total sample budget over all ranks (rsort_multi.cpp kSampleBudget)
+SAMPLE_BUDGET = 1 << 20
+# keys per message of one exchange round (1 GiB of u32): the RCCL of this image (2.26, ROCm 7;
+# torch 2.10) silently leaves the second half of an all_to_all message of >= 2 GiB unwritten
+# (dev/a2a_lab.py: 1 GiB arrives whole, 2 GiB - 4 B does not)
+MAX_PIECE = 1 << 28
+NO_LIMIT = (1 << 62)
 
 
 class GpuOps:
@@ -49,13 +52,13 @@ class GpuOps:
             self._ws = rs.workspace(nbytes, self.device)
         return self._ws
 
-    def top_histogram(self, keys, top_bits, stride=1):
-        h = torch.empty(1 << top_bits, dtype=torch.int32, device=self.device)
-        if stride > 1:
-            rs.top_histogram_sampled(keys, top_bits, stride, h)
-        else:
-            rs.top_histogram(keys, top_bits, h, ws=self._workspace(rs.workspace_size(keys.numel(), top_bits)))
-        return h
+    def sample(self, keys, stride, count, row_len):
+        return rs.sample_device(keys, stride, count, row_len)
+
+    def sort_keys(self, keys):
+        p = rs.plan(keys.numel(), 8, False)
+        rs.sort_device(keys, keys, 8, ws=self._workspace(p.workspace_bytes), plan_=p)
+        return keys
 
     def partition(self, keys, vals, splitters):
         n = keys.numel()
@@ -67,109 +70,93 @@ class GpuOps:
         rs.partition_device(keys, ko, splitters, starts, vals_in=vals, vals_out=vo, ws=self._workspace(need))
         return ko, vo, starts
 
-    def sort(self, keys, vals, k_bits, out_keys=None, out_vals=None):
+    def sort(self, keys, vals, k_bits):
+        """In place."""
         n = keys.numel()
-        ko = out_keys if out_keys is not None else torch.empty_like(keys)
-        vo = None
-        if vals is not None:
-            vo = out_vals if out_vals is not None else torch.empty_like(vals)
         p = rs.plan(n, k_bits, vals is not None)
-        rs.sort_device(keys, ko, k_bits, vals_in=vals, vals_out=vo, ws=self._workspace(p.workspace_bytes), plan_=p)
-        return ko, vo
+        rs.sort_device(keys, keys, k_bits, vals_in=vals, vals_out=vals, ws=self._workspace(p.workspace_bytes),
+                       plan_=p)
+        return keys, vals
 
 
-def choose_splitters(hist: np.ndarray, world: int, top_bits: int) -> list[int]:
-    """world-1 ascending u32 splitters on bin edges of the global top-bits histogram so each
-    rank receives about total/world keys. Bucket i takes the bins up to and including the
-    first bin whose inclusive prefix count reaches (i+1)*total/world."""
-    hist = np.asarray(hist, dtype=np.int64)
-    nbins = hist.size
-    cum = np.cumsum(hist)
-    total = int(cum[-1])
-    shift = 32 - top_bits
-    out: list[int] = []
-    for i in range(1, world):
-        b = int(np.searchsorted(cum, (total * i) // world, side="left"))
-        edge = b + 1
-        s = (edge << shift) if edge < nbins else 0xFFFFFFFF
-        out.append(max(s, out[-1]) if out else s)
-    return out
-
-
-def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, top_bits=12):
+def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, capacity=None):
     """Sort the union of every rank's `keys` (and `vals`); return this rank's slice of the
     global sorted order as (keys, vals, global_offset).
 
     Collectives run on the tensors' device with RCCL ("nccl"); with the gloo backend (tests:
-    several ranks sharing one GPU, or CPU-only ranks) they run on host copies."""
+    several ranks sharing one GPU, or CPU-only ranks) they run on host copies. capacity: the
+    most keys this rank may receive (None: no limit); rs.RSortError(RSORT_ERR_CAPACITY) on every
+    rank alike when any rank's limit would be exceeded."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if ops is None:
         ops = GpuOps(keys.device)
     dev = keys.device
     gloo = dist.get_backend(group) == "gloo"
-    host_comm = gloo and dev.type != "cpu"
-    cdev = torch.device("cpu") if host_comm else dev
+    cdev = torch.device("cpu") if gloo else dev
 
-    def a2a(out, inp, out_splits, in_splits, pieces):
-        """all_to_all of `inp` (segments in_splits, one per destination) into `out` (segments
-        out_splits, one per source), every message cut into `pieces` rounds of <= MAX_MESSAGE."""
-        so = np.concatenate([[0], np.cumsum(in_splits)]).astype(np.int64)
-        ro = np.concatenate([[0], np.cumsum(out_splits)]).astype(np.int64)
-        for q in range(pieces):
-            lo, hi = q * MAX_MESSAGE, (q + 1) * MAX_MESSAGE
-            ins = [inp[so[i] + min(lo, in_splits[i]):so[i] + min(hi, in_splits[i])] for i in range(world)]
-            outs = [out[ro[j] + min(lo, out_splits[j]):ro[j] + min(hi, out_splits[j])] for j in range(world)]
+    def all_gather(t):
+        t = t.to(cdev)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return torch.stack(out)
+
+    n = keys.numel()
+    # 1. key counts -> sampling plan
+    n_all = all_gather(torch.tensor([n], dtype=torch.int64)).cpu().numpy().reshape(-1)
+    sp = rs.multi_sample_plan(n_all.tolist(), max(1, SAMPLE_BUDGET // world))
+
+    # 2. sample, gather, sort: the quantile keys
+    row = ops.sample(keys, sp.stride, sp.count[rank], sp.row_len)
+    q = [0] * (world - 1)
+    gathered = all_gather(row).reshape(-1)
+    if world > 1 and sp.total > 0:
+        srt = ops.sort_keys(gathered.to(dev))
+        srt = srt.cpu().numpy().view(np.uint32)
+        q = [int(srt[rs.multi_quantile_index(sp, i)]) for i in range(1, world)]
+    spl = rs.multi_splitters(world, q)
+
+    # 3-4. stable partition into the splitters' buckets
+    pk, pv, starts = ops.partition(keys, vals, spl.splitters)
+    st = starts.to(torch.int64).cpu().numpy()
+    cnt = (st[1:] - st[:-1]).astype(np.int64)
+    cap = NO_LIMIT if capacity is None else int(capacity)
+
+    # 5. count matrix + capacities -> the exchange plan (identical on every rank)
+    rows = all_gather(torch.from_numpy(np.concatenate([cnt, [cap]]).astype(np.int64))).cpu().numpy()
+    xp = rs.multi_exchange_plan(world, rank, rows[:, :-1], spl, rows[:, -1])
+
+    # 6. the exchange into source-rank order (stability)
+    send_off, send_cnt = list(xp.send_off)[:world], list(xp.send_cnt)[:world]
+    recv_off, recv_cnt = list(xp.recv_off)[:world], list(xp.recv_cnt)[:world]
+    rk = torch.empty(xp.n_recv, dtype=keys.dtype, device=dev)
+    rv = torch.empty(xp.n_recv, dtype=vals.dtype, device=dev) if vals is not None else None
+    rounds = -(-xp.max_message // MAX_PIECE) if xp.max_message > 0 else 0
+    piece = (-(-xp.max_message // rounds) + 63) // 64 * 64 if rounds else 0
+    for src, dst in ((pk, rk), (pv, rv)):
+        if src is None:
+            continue
+        if send_cnt[rank]:
+            dst[recv_off[rank]:recv_off[rank] + recv_cnt[rank]].copy_(src[send_off[rank]:send_off[rank] + send_cnt[rank]])
+        for rd in range(rounds):
+            lo, hi = rd * piece, (rd + 1) * piece
+            ins = [src[send_off[p] + min(lo, send_cnt[p]):send_off[p] + min(hi, send_cnt[p])] if p != rank
+                   else src[:0] for p in range(world)]
+            outs = [dst[recv_off[p] + min(lo, recv_cnt[p]):recv_off[p] + min(hi, recv_cnt[p])] if p != rank
+                    else dst[:0] for p in range(world)]
             if not gloo:
-                dist.all_to_all(outs, ins, group=group)  # RCCL: grouped send/recv of the pieces
+                dist.all_to_all(outs, ins, group=group)  # RCCL: grouped send/recv of this round
                 continue
-            # gloo (tests): one all_to_all_single of the round's pieces on host copies
-            o = torch.empty(sum(int(x.numel()) for x in outs), dtype=out.dtype)
-            dist.all_to_all_single(o, torch.cat([x.cpu() for x in ins]), output_split_sizes=[int(x.numel()) for x in outs],
+            # gloo: one all_to_all_single of the round's pieces on host copies
+            o = torch.empty(sum(int(x.numel()) for x in outs), dtype=dst.dtype)
+            dist.all_to_all_single(o, torch.cat([x.cpu() for x in ins]),
+                                   output_split_sizes=[int(x.numel()) for x in outs],
                                    input_split_sizes=[int(x.numel()) for x in ins], group=group)
             off = 0
             for x in outs:
                 x.copy_(o[off:off + x.numel()])
                 off += x.numel()
-        return out
 
-    # 1-3: global histogram of the top bits (of a 1/SAMPLE_STRIDE block sample: the splitters
-    # only set each rank's load) -> splitters
-    h = ops.top_histogram(keys, top_bits, SAMPLE_STRIDE).to(torch.int64).to(cdev)
-    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-    hist = h.cpu().numpy()
-    splitters = choose_splitters(hist, world, top_bits)
-
-    # 4: stable partition into `world` key ranges
-    pk, pv, starts = ops.partition(keys, vals, splitters)
-    st = starts.to(torch.int64).cpu().numpy()
-    send = (st[1:] - st[:-1]).astype(np.int64)
-
-    # 5: exchange counts
-    send_t = torch.from_numpy(send).to(cdev)
-    recv_t = torch.empty_like(send_t)
-    dist.all_to_all_single(recv_t, send_t, group=group)
-    recv = recv_t.cpu().numpy()
-
-    # 6: exchange keys (and values); chunks arrive in source-rank order (stability). Every rank
-    # needs the same number of rounds: the largest message anywhere, by one small all_reduce.
-    n_recv = int(recv.sum())
-    big = torch.tensor([int(max(send.max(), recv.max()))], dtype=torch.int64, device=cdev)
-    dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
-    pieces = max(1, -(-int(big.item()) // MAX_MESSAGE))
-    rk = torch.empty(n_recv, dtype=keys.dtype, device=dev)
-    a2a(rk, pk, recv.tolist(), send.tolist(), pieces)
-    rv = None
-    if vals is not None:
-        rv = torch.empty(n_recv, dtype=vals.dtype, device=dev)
-        a2a(rv, pv, recv.tolist(), send.tolist(), pieces)
-
-    # 7: local LSD sort of the received bucket
+    # 7. local LSD sort of the received keys
     ok, ov = ops.sort(rk, rv, k_bits)
-
-    # global offset of this rank's slice = keys owned by lower ranks
-    counts = torch.tensor([n_recv], dtype=torch.int64, device=cdev)
-    allc = [torch.zeros_like(counts) for _ in range(world)]
-    dist.all_gather(allc, counts, group=group)
-    offset = int(sum(int(c.item()) for c in allc[:rank]))
-    return ok, ov, offset
+    return ok, ov, int(xp.offset)

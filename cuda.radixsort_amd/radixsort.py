@@ -81,9 +81,52 @@ class PhaseTimes(ctypes.Structure):
                 for i, p in enumerate(PHASES)}
 
 
+MAX_RANKS = 16  # RSORT_MAX_RANKS
+
+
+class SamplePlan(ctypes.Structure):
+    """rsort_sample_plan (include/rsort.h, multi-GPU planning)."""
+    _fields_ = [("world", ctypes.c_int32), ("stride", ctypes.c_int64), ("count", ctypes.c_int64 * MAX_RANKS),
+                ("row_len", ctypes.c_int64), ("total", ctypes.c_int64)]
+
+
+class MultiSplitters(ctypes.Structure):
+    """rsort_multi_splitters."""
+    _fields_ = [("world", ctypes.c_int32), ("nsplit", ctypes.c_int32),
+                ("split", ctypes.c_uint32 * (2 * (MAX_RANKS - 1))), ("cut_bucket", ctypes.c_int32 * MAX_RANKS),
+                ("cut_inside", ctypes.c_int32 * MAX_RANKS)]
+
+    @property
+    def splitters(self) -> list[int]:
+        return [int(self.split[i]) for i in range(self.nsplit)]
+
+
+class ExchangePlan(ctypes.Structure):
+    """rsort_exchange_plan."""
+    _fields_ = [("world", ctypes.c_int32), ("me", ctypes.c_int32),
+                ("send_off", ctypes.c_int64 * MAX_RANKS), ("send_cnt", ctypes.c_int64 * MAX_RANKS),
+                ("recv_off", ctypes.c_int64 * MAX_RANKS), ("recv_cnt", ctypes.c_int64 * MAX_RANKS),
+                ("n_recv", ctypes.c_int64), ("offset", ctypes.c_int64), ("total", ctypes.c_int64),
+                ("max_message", ctypes.c_int64), ("over_capacity", ctypes.c_int32)]
+
+
+_AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                          ctypes.c_void_p)
+_EX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_void_p),
+                          ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p)
+
+
+class Transport(ctypes.Structure):
+    """rsort_transport: the multi-GPU sort's communication plug-in."""
+    _fields_ = [("ctx", ctypes.c_void_p), ("world", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("allgather", _AG_FN), ("exchange", _EX_FN)]
+
+
 # Every symbol include/rsort.h declares, with its ctypes signature.
 _u32p, _vp, _i64, _int, _sz = (ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p, ctypes.c_int64,
                                ctypes.c_int, ctypes.c_size_t)
+_i = _int
 _PP = ctypes.POINTER(Plan)
 SIGNATURES = {
     "rsort_status_string": ([_int], ctypes.c_char_p),
@@ -115,9 +158,22 @@ SIGNATURES = {
     "rsort_multi_workspace_size": ([_i64, _i64, _int, _int, _int], _sz),
     "rsort_u32_multi": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int, _vp,
                          _vp, _sz, _vp], _int),
+    "rsort_multi_sample_plan": ([_i, ctypes.POINTER(_i64), _i64, ctypes.POINTER(SamplePlan)], _int),
+    "rsort_sample_device": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp], _int),
+    "rsort_multi_quantile_index": ([ctypes.POINTER(SamplePlan), _int], _i64),
+    "rsort_multi_splitters_make": ([_int, _u32p, ctypes.POINTER(MultiSplitters)], _int),
+    "rsort_multi_exchange_plan": ([_int, _int, _int, ctypes.POINTER(_i64), ctypes.POINTER(MultiSplitters),
+                                   ctypes.POINTER(_i64), ctypes.POINTER(ExchangePlan)], _int),
+    "rsort_u32_multi_transport": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int,
+                                   ctypes.POINTER(Transport), _vp, _sz, _vp], _int),
+    "rsort_set_exchange_piece": ([_i64], _i64),
+    "rsort_loopback_create": ([_int, ctypes.POINTER(ctypes.c_void_p)], _int),
+    "rsort_loopback_transport": ([ctypes.c_void_p, _int, ctypes.POINTER(Transport)], _int),
+    "rsort_loopback_destroy": ([ctypes.c_void_p], None),
     "rsort_vendor_workspace_size": ([_i64], _sz),
     "rsort_u32_vendor_device": ([_vp, _vp, _i64, _vp, _sz, _vp], _int),
     "rsort_u32_vendor": ([_vp, _vp, _i64], _int),
+    "rsort_fingerprint_device": ([_vp, _vp, _i64, _vp, _vp], _int),
     "rsort_gen_uniform": ([_vp, _i64, ctypes.c_uint64, _vp], _int),
     "rsort_gen_zipf": ([_vp, _i64, ctypes.c_uint64, _vp, _i64, _vp], _int),
     "rsort_gen_iota": ([_vp, _i64, ctypes.c_uint32, _vp], _int),
@@ -368,21 +424,103 @@ class RcclComm:
             self.handle = ctypes.c_void_p()
 
 
-def multi_sort_device(comm: RcclComm, keys, k_bits=8, vals=None, capacity=None, stream=None):
-    """rsort_u32_multi: returns (keys_out[:count], vals_out[:count] or None, global offset)."""
+def default_capacity(n: int) -> int:
+    """Output room per rank for n local keys: balanced output is about the mean count plus the
+    sampling error (~0.1 %); 5/4 n + 64 Ki covers uneven per-rank n up to that."""
+    return int(n + n // 4 + (1 << 16))
+
+
+def multi_sort_device(comm, keys, k_bits=8, vals=None, capacity=None, stream=None, ws=None, out=None):
+    """rsort_u32_multi (comm: RcclComm) or rsort_u32_multi_transport (comm: a Transport):
+    returns (keys_out[:count], vals_out[:count] or None, global offset)."""
     n = keys.numel()
-    cap = int(capacity if capacity is not None else 2 * n + 4096)
+    cap = int(capacity if capacity is not None else default_capacity(n))
     pairs = vals is not None
-    kout = empty_u32(cap, keys.device)
-    vout = empty_u32(cap, keys.device) if pairs else None
-    wsb = int(_lib().rsort_multi_workspace_size(n, cap, k_bits, 1 if pairs else 0, comm.world))
-    ws = workspace(wsb, keys.device)
+    kout, vout = out if out is not None else (empty_u32(cap, keys.device), empty_u32(cap, keys.device) if pairs
+                                               else None)
+    world = comm.world
+    wsb = int(_lib().rsort_multi_workspace_size(n, cap, k_bits, 1 if pairs else 0, world))
+    if ws is None or ws.numel() < wsb:
+        ws = workspace(wsb, keys.device)
     cnt, off = ctypes.c_int64(), ctypes.c_int64()
-    _check(_lib().rsort_u32_multi(_ptr(keys), _ptr(vals), n, _ptr(kout), _ptr(vout), cap, ctypes.byref(cnt),
-                                  ctypes.byref(off), int(k_bits), comm.handle, _ptr(ws), wsb, _stream(stream)),
-           "rsort_u32_multi")
+    if isinstance(comm, Transport):
+        st = _lib().rsort_u32_multi_transport(_ptr(keys), _ptr(vals), n, _ptr(kout), _ptr(vout), cap,
+                                              ctypes.byref(cnt), ctypes.byref(off), int(k_bits), ctypes.byref(comm),
+                                              _ptr(ws), ws.numel(), _stream(stream))
+        _check(st, "rsort_u32_multi_transport")
+    else:
+        _check(_lib().rsort_u32_multi(_ptr(keys), _ptr(vals), n, _ptr(kout), _ptr(vout), cap, ctypes.byref(cnt),
+                                      ctypes.byref(off), int(k_bits), comm.handle, _ptr(ws), ws.numel(),
+                                      _stream(stream)), "rsort_u32_multi")
     c = cnt.value
     return kout[:c], (vout[:c] if pairs else None), off.value
+
+
+def set_exchange_piece(keys: int) -> int:
+    """Largest exchange message per round of rsort_u32_multi* (keys); returns the old value."""
+    return int(_lib().rsort_set_exchange_piece(int(keys)))
+
+
+class LoopbackGroup:
+    """rsort_loopback_*: `world` in-process ranks (one thread each) for the multi-GPU sort."""
+
+    def __init__(self, world: int):
+        self.handle = ctypes.c_void_p()
+        _check(_lib().rsort_loopback_create(int(world), ctypes.byref(self.handle)), "rsort_loopback_create")
+        self.world = world
+
+    def transport(self, rank: int) -> Transport:
+        t = Transport()
+        _check(_lib().rsort_loopback_transport(self.handle, int(rank), ctypes.byref(t)), "rsort_loopback_transport")
+        return t
+
+    def close(self):
+        if self.handle:
+            _lib().rsort_loopback_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+# ---------------------------------------------------------------- multi-GPU planning (host only)
+def multi_sample_plan(n_per_rank, samples_per_rank: int) -> SamplePlan:
+    world = len(n_per_rank)
+    arr = (ctypes.c_int64 * max(1, world))(*[int(x) for x in n_per_rank])
+    sp = SamplePlan()
+    _check(_lib().rsort_multi_sample_plan(world, arr, int(samples_per_rank), ctypes.byref(sp)),
+           "rsort_multi_sample_plan")
+    return sp
+
+
+def sample_device(keys, stride: int, count: int, row_len: int, out=None, stream=None):
+    """rsort_sample_device: the regular splitter sample of the multi-GPU sort (row_len u32)."""
+    out = out if out is not None else empty_u32(row_len, keys.device)
+    _check(_lib().rsort_sample_device(_ptr(keys), keys.numel(), int(stride), int(count), int(row_len), _ptr(out),
+                                      _stream(stream)), "rsort_sample_device")
+    return out
+
+
+def multi_quantile_index(sp: SamplePlan, i: int) -> int:
+    return int(_lib().rsort_multi_quantile_index(ctypes.byref(sp), int(i)))
+
+
+def multi_splitters(world: int, quantile_keys) -> MultiSplitters:
+    q = (ctypes.c_uint32 * max(1, world - 1))(*[int(x) & 0xFFFFFFFF for x in quantile_keys])
+    out = MultiSplitters()
+    _check(_lib().rsort_multi_splitters_make(int(world), q, ctypes.byref(out)), "rsort_multi_splitters_make")
+    return out
+
+
+def multi_exchange_plan(world: int, me: int, counts, spl: MultiSplitters, capacity) -> ExchangePlan:
+    """counts: world x buckets (rows = source ranks); capacity: world entries. Raises RSortError
+    (status 9, RSORT_ERR_CAPACITY) on every rank alike when any rank's output would overflow."""
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    buckets = c.shape[1]
+    cap = np.ascontiguousarray(capacity, dtype=np.int64)
+    out = ExchangePlan()
+    st = _lib().rsort_multi_exchange_plan(int(world), int(me), int(buckets),
+                                          c.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(spl),
+                                          cap.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(out))
+    _check(st, "rsort_multi_exchange_plan")
+    return out
 
 
 def lane_order_probe() -> int:
@@ -467,6 +605,15 @@ def vendor_sort_device(keys_in, keys_out, ws=None, stream=None):
         ws = workspace(need, keys_in.device)
     _check(_lib().rsort_u32_vendor_device(_ptr(keys_in), _ptr(keys_out), n, _ptr(ws), ws.numel(),
                                           _stream(stream)), "rsort_u32_vendor_device")
+
+
+def fingerprint(keys, vals=None, stream=None) -> tuple[int, int]:
+    """rsort_fingerprint_device: (multiset fingerprint, adjacent descents) of keys (+ values)."""
+    out = torch.zeros(2, dtype=torch.int64, device=keys.device)
+    _check(_lib().rsort_fingerprint_device(_ptr(keys), _ptr(vals), keys.numel(), _ptr(out), _stream(stream)),
+           "rsort_fingerprint_device")
+    h, d = out.cpu().tolist()
+    return h & 0xFFFFFFFFFFFFFFFF, d
 
 
 def gen_uniform(out, seed=0x5EED, stream=None):

@@ -1,0 +1,440 @@
+// lines_exp.hip -- development harness (not part of the library): experimental copies of the
+// keys-only rs_scatter_lines pass (cuda.radixsort_amd/csrc/rsort_kernels.hip) with knobs, timed
+// against the library kernel on the same input and checked against its output.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc \
+//         dev/lines_exp.hip -o dev/lines_exp && dev/lines_exp [log2n] [filter]
+// -DLX_STAMPS: per-phase s_memtime stamps of wave 0 (diagnostic build).
+//
+// Knobs (template argument V, bit flags):
+//   1  OUTB   output phase: every quad of a thread read from LDS first, then the segment records,
+//             then the stores (the library reads quad -> waits -> record -> waits -> store)
+//   2  RANK1  rank phase without the per-slot aggregation branch unless the previous tile of the
+//             workgroup saw a per-wave digit count >= 32 (clustered input)
+#define RSORT_LAB_LITE
+#include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+using namespace rsort;
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            printf("HIP error %s at line %d\n", hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+#ifdef LX_STAMPS
+#define LX_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define LX(i)                                                         \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[i] += now_ - st_prev;                                  \
+        st_prev = now_;                                               \
+    } while (0)
+#define LX_FLUSH()                                                                \
+    do {                                                                          \
+        if (threadIdx.x == 0 && a.stamps)                                         \
+            for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 8 + i_] = st_acc[i_]; \
+    } while (0)
+#else
+#define LX_DECL
+#define LX(i)
+#define LX_FLUSH()
+#endif
+
+enum { kOutB = 1, kRank1 = 2 };
+
+template <int BITS, int THREADS, int KPT, int G, int V>
+__global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int W = THREADS / kWave;
+    constexpr int SEG = kWave * KPT;
+    constexpr uint32_t T = THREADS * KPT;
+    constexpr uint32_t TPD = THREADS / R;
+    constexpr uint32_t CAP = T + (G - 1) * R;
+    constexpr uint32_t QPL = G / 4;
+    constexpr uint32_t MAXQ = (CAP / G) * QPL;                      // quads of a full staging area
+    constexpr uint32_t QPT = (MAXQ + THREADS - 1) / THREADS;        // ... per thread
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    static_assert(R <= THREADS && TPD <= kWave && (G == 16 || G == 32), "geometry");
+
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];
+    __shared__ uint32_t s_cnt[W * R + 1];
+    __shared__ uint2 s_out[R];
+    __shared__ uint2 s_flush[R];
+    __shared__ uint32_t s_ws[W];
+    __shared__ uint32_t s_clust[2];
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = t / kWave;
+    const uint32_t lane = lane_id();
+    const uint32_t c = blockIdx.x;
+    const Digit<BITS, kDigitShift> dig{a.shift, 0, nullptr};
+    uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    uint32_t head = 0;
+
+    const uint32_t d_own = t / TPD;
+    const uint32_t sub = t % TPD;
+    const bool leader = sub == 0;
+    uint32_t g_run = 0, carry = 0, inv = 0;
+    if (leader) {
+        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
+        carry = g & (G - 1u);
+        inv = carry;
+        g_run = g;
+        const uint32_t ik = d_own << a.shift;
+        for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = ik;
+    }
+    if (t < 2) s_clust[t] = 0;
+    uint32_t clustered = 1;  // RANK1: the first tile checks
+    uint32_t par = 0;
+
+    const uint32_t base = w * SEG + lane;
+    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT]) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        uint32_t lb = base;
+        asm volatile("" : "+v"(lb));
+        const uint32_t *__restrict__ tk = a.kin + tb + lb;
+        if (valid == T) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = __builtin_nontemporal_load(tk + j * kWave);
+        } else {
+            const uint32_t lim = valid > lb ? valid - lb : 0u;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool in = (uint32_t)(j * kWave) < lim;
+                k[j] = in ? tk[j * kWave] : 0u;
+            }
+        }
+    };
+
+    auto store_quad = [&](uint32_t L, uint32_t q, const u32x4 &kv, const uint2 &info) {
+        const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
+        const uint64_t gp = (uint64_t)(info.x + L * G + q);
+        if (lo <= q) {
+            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
+        } else {
+#pragma unroll
+            for (uint32_t x = 0; x < 4; ++x)
+                if (lo <= q + x) a.kout[gp + x] = kv[x];
+        }
+    };
+
+    uint32_t key[KPT];
+    if (cbeg < cend) load_tile(cbeg, key);
+    __syncthreads();
+
+    LX_DECL
+    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const bool full = valid == T && head == 0;
+        const uint64_t nb = tb + T;
+        uint32_t plim = valid > base ? valid - base : 0u;
+        asm volatile("" : "+v"(plim));
+        const bool h0 = base >= head;
+        head = 0;
+        LX(0);
+#pragma unroll
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+        uint32_t rk[(KPT + 1) / 2];
+        uint32_t nkey[KPT];
+        if (full) {
+            if ((V & kRank1) && !clustered) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t dj = dig(key[j]);
+                    const uint32_t r = atomicAdd(&s_cnt[w * R + dj], 1u);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t dj = dig(key[j]);
+                    const uint32_t r = rank_add(&s_cnt[w * R], dj);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = dig(key[j]);
+                uint32_t r = 0;
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            }
+        }
+        if (nb < cend) load_tile(nb, nkey);
+        __syncthreads();
+        LX(1);
+
+        constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
+        uint32_t part = 0;
+        uint32_t wx[WPT];
+        bool hot = false;
+        if (sub < (uint32_t)W) {
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * R + d_own] : 0u;
+                part += wx[i];
+                hot |= wx[i] >= 32u;
+            }
+        }
+        if constexpr ((V & kRank1) != 0) {
+            // slot par: set by any wave that saw a hot per-wave digit count, read after the barrier
+            // below; slot par ^ 1 is reset for the next tile (its readers are a barrier behind)
+            if (__ballot(hot) != 0 && lane == 0) s_clust[par] = 1;
+            if (t == 0) s_clust[par ^ 1u] = 0;
+        }
+        uint32_t gpre, cnt;
+        group_scan<TPD>(part, sub, gpre, cnt);
+        uint32_t wcnt = 0, A = 0, e = 0;
+        if (leader) {
+            A = g_run - carry;
+            e = g_run + cnt;
+            wcnt = max(A, e & ~(uint32_t)(G - 1)) - A;
+        }
+        uint32_t nseg;
+        const uint32_t S = block_excl_scan1<THREADS>(wcnt, s_ws, nseg);
+        LX(2);
+        const uint32_t gS = group_lane<TPD>(S, 0), gw = group_lane<TPD>(wcnt, 0);
+        const uint32_t gA = group_lane<TPD>(A, 0), gc = group_lane<TPD>(carry, 0), ginv = group_lane<TPD>(inv, 0);
+        {
+            const uint32_t d = d_own;
+            if (sub < (uint32_t)W) {
+                uint32_t acc = gS + gc + gpre;
+#pragma unroll
+                for (uint32_t i = 0; i < WPT; ++i) {
+                    const uint32_t v = sub * WPT + i;
+                    if (v < (uint32_t)W) s_cnt[v * R + d] = acc | ((gS + gw) << 16);
+                    acc += wx[i];
+                }
+            }
+            constexpr uint32_t CB = G / TPD;
+            static_assert(G % TPD == 0 && CB % 4 == 0, "quad carries");
+            const uint32_t x0 = sub * CB;
+            if (gw > 0 && x0 < gc) {
+                u32x4 ck[CB / 4];
+#pragma unroll
+                for (uint32_t i = 0; i < CB / 4; ++i)
+                    ck[i] = *reinterpret_cast<const u32x4 *>(&s_stage[CAP + d * G + x0 + 4 * i]);
+#pragma unroll
+                for (uint32_t i = 0; i < CB / 4; ++i) {
+                    const uint32_t x = x0 + 4 * i;
+                    if (x + 4 <= gc) {
+                        *reinterpret_cast<u32x4 *>(&s_stage[gS + x]) = ck[i];
+                    } else if (x < gc) {
+#pragma unroll
+                        for (uint32_t e2 = 0; e2 < 4; ++e2)
+                            if (x + e2 < gc) s_stage[gS + x + e2] = ck[i][e2];
+                    }
+                }
+            }
+            if (leader) {
+                s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
+                if (gw > 0) inv = 0;
+                carry = e - (A + gw);
+                g_run = e;
+                if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
+            }
+        }
+        LX(3);
+        __syncthreads();
+        if constexpr ((V & kRank1) != 0) {
+            clustered = s_clust[par];
+            par ^= 1u;
+        }
+        LX(4);
+
+        constexpr int SB = KPT < 8 ? KPT : 8;
+#pragma unroll
+        for (int j0 = 0; j0 < KPT; j0 += SB) {
+            uint32_t pp[SB], ll[SB], dd[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                asm volatile("" : "+v"(key[j]));
+                dd[u] = dig(key[j]);
+                const uint32_t bl = s_cnt[w * R + dd[u]];
+                pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+                ll[u] = bl >> 16;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                uint32_t idx = pp[u] < ll[u] ? pp[u] : CAP + dd[u] * G + (pp[u] - ll[u]);
+                if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + R * G;
+                s_stage[idx] = key[j];
+            }
+        }
+        __syncthreads();
+        LX(5);
+
+        const uint32_t nq = (nseg / G) * QPL;
+        if constexpr ((V & kOutB) != 0) {
+            u32x4 kv[QPT];
+            uint2 info[QPT];
+#pragma unroll
+            for (uint32_t i = 0; i < QPT; ++i) {
+                const uint32_t item = t + i * THREADS;
+                if (item < nq) kv[i] = *reinterpret_cast<const u32x4 *>(&s_stage[(item / QPL) * G + (item % QPL) * 4]);
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < QPT; ++i) {
+                const uint32_t item = t + i * THREADS;
+                if (item < nq) info[i] = s_out[dig(kv[i].x)];
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < QPT; ++i) {
+                const uint32_t item = t + i * THREADS;
+                if (item < nq) store_quad(item / QPL, (item % QPL) * 4, kv[i], info[i]);
+            }
+        } else {
+#pragma unroll 2
+            for (uint32_t item = t; item < nq; item += THREADS) {
+                const uint32_t L = item / QPL, q = (item % QPL) * 4u;
+                const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_stage[L * G + q]);
+                store_quad(L, q, kv, s_out[dig(kv.x)]);
+            }
+        }
+        LX(6);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) key[j] = nkey[j];
+    }
+    if (cbeg < cend) {
+        for (uint32_t item = t; item < R * G; item += THREADS) {
+            const uint2 fl = s_flush[item / G];
+            const uint32_t x = item % G;
+            if ((fl.y & 0xFFu) <= x && x < (fl.y >> 8)) a.kout[(uint64_t)fl.x + x] = s_stage[CAP + item];
+        }
+    }
+    LX_FLUSH();
+}
+
+__global__ void count_mismatch(const uint32_t *a, const uint32_t *b, uint64_t n, unsigned long long *bad) {
+    unsigned long long local = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        local += a[i] != b[i];
+    if (local) atomicAdd(bad, local);
+}
+
+struct Ctx {
+    uint64_t n;
+    uint32_t *keys, *out, *ref, *table, *bsums;
+    unsigned long long *bad, *stamps;
+    int cus;
+    hipEvent_t e0, e1;
+    bool have_ref = false;
+};
+
+static const char *g_filter = nullptr;
+
+template <int BITS, int THREADS, int KPT, typename K>
+void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
+    if (g_filter && !strstr(name, g_filter)) return;
+    int bpc = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, kern, THREADS, 0));
+    const uint64_t T = (uint64_t)THREADS * KPT;
+    const uint64_t tiles = (c.n + T - 1) / T;
+    const uint64_t target = (uint64_t)c.cus * bpc;
+    const uint64_t tpc = (tiles + target - 1) / target;
+    const uint64_t chunks = (tiles + tpc - 1) / tpc;
+    HistArgs h{};
+    h.keys = c.keys;
+    h.table = c.table;
+    h.n = c.n;
+    h.chunk_keys = tpc * T;
+    h.num_chunks = (uint32_t)chunks;
+    h.shift = shift;
+    h.vec = 1;
+    h.split = 1;
+    CK(launch_histogram(BITS, kDigitShift, h, 0));
+    ScanArgs s{};
+    s.table = c.table;
+    s.block_sums = c.bsums;
+    s.m = (uint64_t)chunks << BITS;
+    s.nblocks = (uint32_t)((s.m + kScanSegment - 1) / kScanSegment);
+    CK(launch_scan(s, 0));
+    ScatterArgs a{};
+    a.kin = c.keys;
+    a.kout = c.out;
+    a.table = c.table;
+    a.n = c.n;
+    a.chunk_keys = tpc * T;
+    a.num_chunks = (uint32_t)chunks;
+    a.shift = shift;
+    a.stamps = c.stamps;
+    CK(hipMemset(c.out, 0, c.n * 4));
+    kern<<<chunks, THREADS>>>(a);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(c.e0, 0));
+    for (int i = 0; i < reps; ++i) kern<<<chunks, THREADS>>>(a);
+    CK(hipEventRecord(c.e1, 0));
+    CK(hipEventSynchronize(c.e1));
+    CK(hipGetLastError());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, c.e0, c.e1));
+    ms /= reps;
+    unsigned long long bad = 0;
+    if (!c.have_ref) {
+        CK(hipMemcpy(c.ref, c.out, c.n * 4, hipMemcpyDeviceToDevice));
+        c.have_ref = true;
+    } else {
+        CK(hipMemset(c.bad, 0, 8));
+        count_mismatch<<<4096, 256>>>(c.out, c.ref, c.n, c.bad);
+        CK(hipMemcpy(&bad, c.bad, 8, hipMemcpyDeviceToHost));
+    }
+    printf("%-40s chunks=%-5llu tpc=%-4llu %8.3f ms %7.1f GB/s %5.1f%%  mismatch=%llu\n", name,
+           (unsigned long long)chunks, (unsigned long long)tpc, ms, 8.0 * c.n / ms / 1e6, 8.0 * c.n / ms / 1e6 / 80.0, bad);
+#ifdef LX_STAMPS
+    std::vector<unsigned long long> st(chunks * 8);
+    CK(hipMemcpy(st.data(), c.stamps, chunks * 8 * 8, hipMemcpyDeviceToHost));
+    double sum[8] = {0};
+    for (uint64_t b = 0; b < chunks; ++b)
+        for (int i = 0; i < 8; ++i) sum[i] += st[b * 8 + i];
+    const char *names[8] = {"loop", "1:rank+bar", "2:scan", "2:bases+carry", "2:bar", "3:stage+bar", "4:out", "-"};
+    printf("    cycles per tile (wave 0):");
+    for (int i = 0; i < 7; ++i) printf(" %s=%.0f", names[i], sum[i] / chunks / tpc);
+    printf("\n");
+#endif
+    fflush(stdout);
+}
+
+int main(int argc, char **argv) {
+    Ctx c{};
+    const int lg = argc > 1 ? atoi(argv[1]) : 30;
+    g_filter = argc > 2 ? argv[2] : nullptr;
+    c.n = 1ull << lg;
+    CK(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, 0));
+    CK(hipMalloc(&c.keys, c.n * 4));
+    CK(hipMalloc(&c.out, c.n * 4));
+    CK(hipMalloc(&c.ref, c.n * 4));
+    CK(hipMalloc(&c.table, (c.n / 1024 + 65536) * 4 * 16));
+    CK(hipMalloc(&c.bsums, 1 << 24));
+    CK(hipMalloc(&c.bad, 8));
+    CK(hipMalloc(&c.stamps, 65536 * 8 * 8));
+    CK(hipEventCreate(&c.e0));
+    CK(hipEventCreate(&c.e1));
+    CK(launch_gen_uniform(c.keys, c.n, 0x5EED, 0));
+    CK(hipDeviceSynchronize());
+    printf("n=%llu cus=%d\n", (unsigned long long)c.n, c.cus);
+    for (int rep = 0; rep < 2; ++rep) {
+        run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>",
+                         rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, true, 0, 3>, 0);
+        run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, 0);
+        run<8, 1024, 16>(c, "lx outb", lx_lines<8, 1024, 16, 32, kOutB>, 0);
+        run<8, 1024, 16>(c, "lx rank1", lx_lines<8, 1024, 16, 32, kRank1>, 0);
+        run<8, 1024, 16>(c, "lx outb+rank1", lx_lines<8, 1024, 16, 32, kOutB | kRank1>, 0);
+    }
+    return 0;
+}

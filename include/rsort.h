@@ -208,22 +208,126 @@ RSORT_API int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bit
 RSORT_API int rsort_top_histogram_sampled(const uint32_t *d_keys, int64_t n, int top_bits,
                                           int stride, uint32_t *d_hist, void *stream);
 
-/* ---------------------------------------------------------------- multi-GPU sort (RCCL) */
-/* One rank per GPU over an RCCL communicator (`nccl_comm` is an ncclComm_t; the
- * reference is single-GPU, Parallel7.cu:10). Every rank passes its n local keys (and values);
- * on return rank r's d_keys_out[0 .. *out_n) holds the keys of global ranks
- * [*out_offset, *out_offset + *out_n) of the sorted union, i.e. concatenating the ranks' outputs
- * in rank order gives Baseline1's result; pairs stay stable (source-rank order). Steps:
- * top-12-bit histogram -> ncclAllReduce -> splitters -> stable partition into `world` key
- * ranges -> ncclAllGather of the count matrix -> one grouped ncclSend/ncclRecv exchange ->
- * local LSD sort. Synchronises `stream` twice (bucket sizes are needed on the host).
- * capacity: room in d_keys_out / d_vals_out (RSORT_ERR_CAPACITY if exceeded; a balanced input
- * needs about n). Up to 16 ranks. */
+/* ---------------------------------------------------------------- multi-GPU planning (host only) */
+/* The host-side decisions of the multi-GPU sort, as pure functions (no device, no communicator):
+ * rsort_u32_multi* and cuda.radixsort_amd/multi.py both call them, and tests drive them on the
+ * CPU at any world size. Every rank calls them with the same gathered inputs and gets the same
+ * answer, so the ranks agree on every decision (including errors) without another collective.
+ *
+ * 1. Sampling. Given every rank's key count, the sampling stride (the same on every rank) and
+ *    each rank's sample count: rank r samples key[min(n_r - 1, j * stride + stride / 2)] for
+ *    j < count[r] and pads its row to row_len with 0xFFFFFFFF. Every sample then stands for
+ *    `stride` keys, so the sorted union of the rows gives the global quantiles directly: the
+ *    i-th of world - 1 splitters is sorted[floor(i * total_samples / world)]. */
+#define RSORT_MAX_RANKS 16
+typedef struct rsort_sample_plan {
+    int32_t world;
+    int64_t stride;                  /* keys per sample, >= 1 */
+    int64_t count[RSORT_MAX_RANKS];  /* samples taken by each rank */
+    int64_t row_len;                 /* samples per rank in the gathered buffer (max count, >= 1) */
+    int64_t total;                   /* sum of count */
+} rsort_sample_plan;
+RSORT_API int rsort_multi_sample_plan(int world, const int64_t *n_per_rank, int64_t samples_per_rank,
+                                      rsort_sample_plan *out);
+/* The device side of step 1: d_out[j] = d_keys[min(n - 1, j * stride + stride / 2)] for j < count,
+ * 0xFFFFFFFF for count <= j < row_len. */
+RSORT_API int rsort_sample_device(const uint32_t *d_keys, int64_t n, int64_t stride, int64_t count,
+                                  int64_t row_len, uint32_t *d_out, void *stream);
+/* Index into the sorted gathered samples of splitter i (1 <= i < world). */
+RSORT_API int64_t rsort_multi_quantile_index(const rsort_sample_plan *sp, int i);
+
+/* 2. Splitters. From the world - 1 quantile keys v_1 <= ... <= v_{world-1}: the partition's
+ * splitters and, for each rank boundary, where it cuts. For world <= 8 every distinct v gets a
+ * bucket of its own, [v, v + 1) ("equal keys"), between the buckets of the keys below and above
+ * it, and boundary r cuts INSIDE the equal-keys bucket of v_r at the position that balances the
+ * ranks: a run of equal keys (a hot key, duplicate-heavy input) is split across ranks in global
+ * (source rank, position) order, which keeps the sort stable. For world > 8 the 2 * (world - 1)
+ * splitters would exceed the partition's 16 buckets: the splitters are the v's themselves and
+ * boundaries cut on bucket edges. */
+typedef struct rsort_multi_splitters {
+    int32_t world;
+    int32_t nsplit;                                 /* partition splitters (buckets = nsplit + 1) */
+    uint32_t split[2 * (RSORT_MAX_RANKS - 1)];      /* non-decreasing */
+    int32_t cut_bucket[RSORT_MAX_RANKS];            /* boundary r (1..world-1) lies in this bucket */
+    int32_t cut_inside[RSORT_MAX_RANKS];            /* 1: anywhere inside it (equal keys); 0: at its start */
+} rsort_multi_splitters;
+RSORT_API int rsort_multi_splitters_make(int world, const uint32_t *quantile_keys, rsort_multi_splitters *out);
+
+/* 3. Exchange. counts[s * buckets + b] = keys of rank s's partition in bucket b (the row every
+ * rank gathers after partitioning); capacity[r] = output room of rank r. For rank `me`: what it
+ * sends to each rank (offset and count in its partitioned buffer), what it receives from each
+ * rank (in source-rank order: offset and count in its output), its output count and global
+ * offset. RSORT_ERR_CAPACITY (with over_capacity = the first rank concerned) when ANY rank would
+ * receive more than its capacity -- every rank sees the same matrix, so all ranks return it
+ * together, before any key moves. */
+typedef struct rsort_exchange_plan {
+    int32_t world, me;
+    int64_t send_off[RSORT_MAX_RANKS], send_cnt[RSORT_MAX_RANKS];
+    int64_t recv_off[RSORT_MAX_RANKS], recv_cnt[RSORT_MAX_RANKS];
+    int64_t n_recv;        /* keys this rank ends with */
+    int64_t offset;        /* global rank of its first key */
+    int64_t total;         /* keys over all ranks */
+    int64_t max_message;   /* largest message between two different ranks, anywhere (keys) */
+    int32_t over_capacity; /* -1, or the lowest rank whose output would overflow */
+} rsort_exchange_plan;
+RSORT_API int rsort_multi_exchange_plan(int world, int me, int buckets, const int64_t *counts,
+                                        const rsort_multi_splitters *sp, const int64_t *capacity,
+                                        rsort_exchange_plan *out);
+
+/* ---------------------------------------------------------------- multi-GPU sort */
+/* One rank per GPU (the reference is single-GPU, Parallel7.cu:10). Every rank
+ * passes its n local keys (and values); on return rank r's d_keys_out[0 .. *out_n) holds the keys
+ * of global ranks [*out_offset, *out_offset + *out_n) of the sorted union, i.e. concatenating the
+ * ranks' outputs in rank order gives Baseline1's result; pairs stay stable (equal keys keep their
+ * (source rank, position) order). Steps: all-gather of the key counts -> a regular sample of the
+ * keys, all-gathered and sorted on the device -> world - 1 quantile keys -> splitters with a
+ * bucket of its own for each quantile key (world <= 8), so a run of equal keys is split across
+ * ranks -> stable partition -> all-gather of the bucket counts and capacities -> the exchange
+ * plan (the same on every rank) -> one exchange (own range by a device copy, the rest point to
+ * point in rounds of <= 2^28 keys per message) -> local LSD sort. Synchronises `stream` four
+ * times (counts are needed on the host).
+ * capacity: room in d_keys_out / d_vals_out. RSORT_ERR_CAPACITY when ANY rank would receive more
+ * than its capacity: every rank returns it, before any key moves (balanced output needs about
+ * total / world plus the sampling error, ~0.1 %). Up to RSORT_MAX_RANKS ranks. */
 RSORT_API size_t rsort_multi_workspace_size(int64_t n, int64_t capacity, int k_bits, int pairs, int world);
+/* Over an RCCL communicator (`nccl_comm` is an ncclComm_t; RCCL result codes are all checked,
+ * RSORT_ERR_COMM on failure). */
 RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n,
                               uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t capacity,
                               int64_t *out_n, int64_t *out_offset, int k_bits, void *nccl_comm,
                               void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* Largest message of one exchange round, in keys (default and maximum 2^28 = 1 GiB; >= 64).
+ * Process-wide; returns the previous value. Tests set small values to force several rounds. */
+RSORT_API int64_t rsort_set_exchange_piece(int64_t keys);
+
+/* The communication the multi-GPU sort needs, as a plug-in (RCCL is one implementation, the
+ * in-process loopback below another; MPI or a host transport could be a third). Both calls are
+ * made by every rank in the same order; they return 0 or a nonzero rsort_status. */
+typedef struct rsort_transport {
+    void *ctx;
+    int32_t world, rank;
+    /* every rank contributes `bytes` device bytes at d_send; d_recv (world * bytes) receives the
+     * contributions in rank order. Stream-ordered on `stream` (or synchronous). */
+    int (*allgather)(void *ctx, const void *d_send, void *d_recv, size_t bytes, void *stream);
+    /* one round of messages: for each peer p != rank, send send_bytes[p] bytes from d_send[p] and
+     * receive recv_bytes[p] bytes into d_recv[p] (0 = none; entry `rank` is always 0). */
+    int (*exchange)(void *ctx, void *const *d_send, const size_t *send_bytes, void *const *d_recv,
+                    const size_t *recv_bytes, void *stream);
+} rsort_transport;
+RSORT_API int rsort_u32_multi_transport(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n,
+                                        uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t capacity,
+                                        int64_t *out_n, int64_t *out_offset, int k_bits,
+                                        const rsort_transport *transport, void *d_workspace,
+                                        size_t workspace_bytes, void *stream);
+/* In-process loopback world: `world` ranks, one host thread each, calling
+ * rsort_u32_multi_transport concurrently on their own streams (one device, or devices with peer
+ * access). Collectives are a host rendezvous plus device-to-device copies; a rank that waits more
+ * than 120 s fails with RSORT_ERR_COMM (and so do the others). For testing the multi-GPU path on
+ * one GPU (RCCL refuses two ranks on one device). */
+RSORT_API int rsort_loopback_create(int world, void **group);
+RSORT_API int rsort_loopback_transport(void *group, int rank, rsort_transport *out);
+RSORT_API void rsort_loopback_destroy(void *group);
 
 /* ---------------------------------------------------------------- vendor comparator */
 /* rocPRIM's device radix sort (what sortByThrust resolves to on ROCm), for the
@@ -232,6 +336,14 @@ RSORT_API size_t rsort_vendor_workspace_size(int64_t n);
 RSORT_API int rsort_u32_vendor_device(const uint32_t *d_in, uint32_t *d_out, int64_t n,
                                       void *d_workspace, size_t workspace_bytes, void *stream);
 RSORT_API int rsort_u32_vendor(const uint32_t *in, uint32_t *out, int64_t n);
+
+/* ---------------------------------------------------------------- output check */
+/* d_out[0] = sum over i of fmix64(d_vals[i] << 32 | d_keys[i]) mod 2^64 (d_vals may be NULL: 0),
+ * an order-independent fingerprint of the (key, value) multiset; d_out[1] = #{i : d_keys[i] >
+ * d_keys[i + 1]}. A correct sort keeps d_out[0] and has d_out[1] == 0 (bench.py checks its timed
+ * output this way; the parity tests compare with the oracle instead). d_out: 2 u64, device. */
+RSORT_API int rsort_fingerprint_device(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n,
+                                       uint64_t *d_out, void *stream);
 
 /* ---------------------------------------------------------------- synthetic workloads */
 /* key[i] = high 32 bits of splitmix64(seed + i). */

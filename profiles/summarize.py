@@ -71,6 +71,12 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
     for (kn, c), vs in sorted(fetch.items()) + sorted(write.items()):
         rows.setdefault(kn, {})[c + "_KiB_per_launch"] = sum(vs) / len(vs)
         rows[kn]["launches_" + c] = len(vs)
+    # the rocprofv3 --stats average duration of the same scatter kernel (bench.py reports the
+    # roofline fraction from it next to its own HIP-event figure)
+    rp_avg, rp_calls = None, 0
+    for r in csv.DictReader(open(stats)):
+        if r["Name"] in names or (not names and "rs_scatter" in r["Name"]):
+            rp_avg, rp_calls = float(r["AverageNs"]), int(r["Calls"])
     path = HERE / f"{tag}_pmc.json"
     prev = json.loads(path.read_text()) if path.exists() else {}
     cfg = f"n{n}_k{k}_{dist}_{'pairs' if pairs else 'keys'}_match:{kernel}"
@@ -94,6 +100,9 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
                 "algorithmic_bytes_per_launch": algo,
                 "traffic_over_algorithmic": (read_bytes + write_bytes) / algo,
                 "calibration": {"fetch_ratio": round(fetch_ratio, 4), "write_ratio": round(write_ratio, 4)},
+                "rocprof_avg_ns": rp_avg,
+                "rocprof_calls": rp_calls,
+                "rocprof_source": f"profiles/{stats_tag or tag}_kernel_stats.csv",
             }
         },
         "per_kernel_raw": {**prev.get("per_kernel_raw", {}), cfg: rows},

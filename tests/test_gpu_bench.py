@@ -22,10 +22,14 @@ def run_bench(*args):
 
 
 def test_bench_headline_contract():
-    d = run_bench("--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--cpu-n", str(1 << 20), "--cpu-reps", "1")
+    d = run_bench("--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--cpu-n", str(1 << 20), "--cpu-reps", "1",
+                  "--cpu-rows", "18,24")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "vendor", "end_to_end"):
         assert k in d, k
+    assert d["verified"] is True  # the timed output: sorted, same multiset as the input
+    assert d["vendor"]["value"] > 0 and d["end_to_end"]["ms_per_sort"] > 0
+    assert set(d["cpu_baseline"]["rows"]) == {"2^18", "2^24"}
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["scaling"] == "weak" and d["dtype"] == "u32" and d["value"] > 0
     assert "workload" in d["config"]
@@ -47,5 +51,12 @@ def test_bench_primitives_and_dist_path():
     d = run_bench("--primitives", "--steps", "2", "--warmup", "1", "--keys", str(1 << 24))
     for k in ("copy", "histogram", "scan", "scatter", "local_sort", "partition_8"):
         assert d["primitives"][k]["ms"] > 0, k
-    d = run_bench("--dist-path", "--steps", "1", "--warmup", "1", "--keys", str(1 << 24), "--no-cpu")
-    assert d["value"] > 0 and "range-partition" in d["config"]["parallelism"]
+    for impl in ("c", "torch"):
+        d = run_bench("--dist-path", "--dist-impl", impl, "--steps", "1", "--warmup", "1", "--keys", str(1 << 24),
+                      "--no-cpu")
+        assert d["value"] > 0 and "range-partition" in d["config"]["parallelism"] and d["verified"] is True
+
+
+def test_bench_pairs_zipf_verified():
+    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 24), "--dist", "zipf", "--pairs", "--no-cpu")
+    assert d["verified"] is True and d["config"]["pairs"] is True

@@ -129,7 +129,12 @@ def _c_multi_worker(rank, world, uid_path, out_dir, n, pairs):
     import radixsort as rs
     torch.cuda.set_device(0)
     uid = Path(uid_path).read_bytes()
-    comm = rs.RcclComm(world, rank, uid)
+    try:
+        comm = rs.RcclComm(world, rank, uid)
+    except rs.RSortError as e:
+        # RCCL refuses two ranks on one device ("Duplicate GPU detected"): recorded, not hidden
+        Path(out_dir, f"refused{rank}").write_text(str(e))
+        return
     try:
         keys, vals = _inputs(rank, n, "zipf", pairs)
         ok, ov, off = rs.multi_sort_device(comm, rs.from_numpy_u32(keys), 8,
@@ -144,8 +149,10 @@ def _c_multi_worker(rank, world, uid_path, out_dir, n, pairs):
 
 
 def test_c_multi_two_ranks_one_gpu(tmp_path):
-    """Two RCCL ranks on one GPU (the pool's boxes have one): the exchange logic of the 8-GPU
-    path with real kernels. Skipped if RCCL refuses two ranks on one device."""
+    """Two RCCL ranks on one GPU. This RCCL refuses that at ncclCommInitRank ("Duplicate GPU
+    detected : rank 0 and rank 1 both on CUDA device"), the only case that skips; any other
+    failure (a crash, an error status, a wrong result) fails. The world > 1 C-ABI path itself is
+    covered on this box by the loopback transport tests below."""
     sys.path.insert(0, str(PKG))
     import radixsort as rs
     uid_path = tmp_path / "uid"
@@ -158,11 +165,13 @@ def test_c_multi_two_ranks_one_gpu(tmp_path):
         p.start()
     for p in procs:
         p.join(timeout=240)
-    if any(p.exitcode != 0 for p in procs):
-        for p in procs:
-            if p.is_alive():
-                p.kill()
-        pytest.skip(f"RCCL with {world} ranks on one GPU unavailable (exit codes {[p.exitcode for p in procs]})")
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    refused = sorted(tmp_path.glob("refused*"))
+    if refused:
+        pytest.skip(f"RCCL refuses {world} ranks on one GPU: {refused[0].read_text()[:200]}")
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     all_k, all_v = zip(*[_inputs(r, n, "zipf", pairs) for r in range(world)])
     got = [np.load(tmp_path / f"k{r}.npy") for r in range(world)]
     offs = [int(np.load(tmp_path / f"o{r}.npy")[0]) for r in range(world)]
@@ -170,6 +179,100 @@ def test_c_multi_two_ranks_one_gpu(tmp_path):
     rk, rv = oracle_sort_pairs(np.concatenate(all_k), np.concatenate(all_v), 8)
     assert np.array_equal(np.concatenate(got), rk)
     assert np.array_equal(np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)]), rv)
+
+
+# ------------------------------------------------------------------ C ABI at world > 1: loopback transport
+def _loopback_inputs(rank, n, dist_name, pairs):
+    keys, vals = _inputs(rank, n, "zipf" if dist_name == "zipf" else "uniform", pairs)
+    if dist_name == "hot":
+        keys = keys.copy()
+        keys[: keys.size * 3 // 4] = 0xC0FFEE  # one key: 3/4 of every rank's keys
+    elif dist_name == "equal":
+        keys = np.full(keys.size, 12345, np.uint32)
+    elif dist_name == "empty0" and rank == 0:
+        keys = keys[:0]
+        vals = vals[:0] if vals is not None else None
+    return keys, vals
+
+
+def _run_loopback(world, inputs, k, capacity=None, piece=None):
+    """world threads in this process, one stream each, calling rsort_u32_multi_transport with
+    the loopback transport on cuda:0 concurrently. Returns per-rank (keys, vals, offset) or the
+    per-rank RSortError statuses."""
+    import threading
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    torch.cuda.set_device(0)
+    if capacity is None:
+        capacity = sum(int(i[0].size) for i in inputs) + 1
+    grp = rs.LoopbackGroup(world)
+    old_piece = rs.set_exchange_piece(piece) if piece else None
+    dev_in = [(rs.from_numpy_u32(kx), rs.from_numpy_u32(vx) if vx is not None else None) for kx, vx in inputs]
+    res = [None] * world
+
+    def run(r):
+        torch.cuda.set_device(0)
+        st = torch.cuda.Stream()
+        try:
+            with torch.cuda.stream(st):
+                kk, vv = dev_in[r]
+                ok, ov, off = rs.multi_sort_device(grp.transport(r), kk, k, vals=vv, capacity=capacity,
+                                                   stream=st)
+                st.synchronize()
+                res[r] = (rs.to_numpy_u32(ok), rs.to_numpy_u32(ov) if ov is not None else None, off)
+        except rs.RSortError as e:
+            res[r] = e.status
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    alive = any(t.is_alive() for t in th)
+    if old_piece:
+        rs.set_exchange_piece(old_piece)
+    if not alive:
+        grp.close()
+    assert not alive, "loopback ranks did not finish"
+    return res
+
+
+@pytest.mark.parametrize("world,dist_name,pairs,k,piece", [(2, "uniform", False, 8, None), (2, "zipf", True, 8, None),
+                                                           (3, "hot", True, 8, 4096), (4, "equal", False, 8, None),
+                                                           (4, "uniform", True, 4, 10000), (8, "zipf", False, 8, None),
+                                                           (3, "empty0", True, 8, None)])
+def test_c_multi_loopback(world, dist_name, pairs, k, piece):
+    """rsort_u32_multi_transport at world 2..8 with the real kernels (sampling, device sort of the
+    gathered sample, partition into equal-key buckets, exchange plan, exchange, in-place local
+    sort): the ranks' outputs concatenated in rank order equal Baseline1 on the union of the
+    inputs (stable with values), offsets are the exclusive scan of the counts, and every rank
+    holds the mean count within 5 % -- also when one key holds 3/4 of the keys. piece: keys per
+    exchange message (rsort_set_exchange_piece), small to force many rounds."""
+    n = 300_000
+    inputs = [_loopback_inputs(r, n, dist_name, pairs) for r in range(world)]
+    res = _run_loopback(world, inputs, k, piece=piece)
+    assert all(isinstance(x, tuple) for x in res), res
+    got = [x[0] for x in res]
+    offs = [x[2] for x in res]
+    assert offs == list(np.cumsum([0] + [g.size for g in got[:-1]]))
+    keys = np.concatenate([i[0] for i in inputs])
+    if pairs:
+        rk, rv = oracle_sort_pairs(keys, np.concatenate([i[1] for i in inputs]), k)
+        assert np.array_equal(np.concatenate(got), rk)
+        assert np.array_equal(np.concatenate([x[1] for x in res]), rv)
+    else:
+        assert np.array_equal(np.concatenate(got), oracle_sort(keys, k))
+    sizes = np.array([g.size for g in got])
+    assert np.abs(sizes - keys.size / world).max() <= 0.05 * keys.size / world + 64, sizes
+
+
+def test_c_multi_loopback_capacity_on_every_rank():
+    """one rank's output too small -> EVERY rank returns RSORT_ERR_CAPACITY
+    before any key moves (no rank is left waiting in the exchange)."""
+    world = 3
+    inputs = [_loopback_inputs(r, 100_000, "uniform", False) for r in range(world)]
+    res = _run_loopback(world, inputs, 8, capacity=50_000)  # each rank would receive ~100 000
+    assert res == [9] * world
 
 
 # ------------------------------------------------------------------ >= 2 GiB exchange messages

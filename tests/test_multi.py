@@ -37,11 +37,17 @@ def _t(a):
 class NumpyOps:
     """CPU stand-in for multi.GpuOps with the kernels' exact semantics (test-only)."""
 
-    def top_histogram(self, keys, top_bits, stride=1):
+    def sample(self, keys, stride, count, row_len):
+        # rsort_sample_device: key[min(n - 1, j * stride + stride / 2)] for j < count, then padding
         k = _u32(keys)
-        if stride > 1:  # rsort_top_histogram_sampled: every stride-th block of 256 keys
-            k = k[(np.arange(k.size) // 256) % stride == 0]
-        return torch.from_numpy(np.bincount(k >> np.uint32(32 - top_bits), minlength=1 << top_bits).astype(np.int32))
+        out = np.full(row_len, 0xFFFFFFFF, np.uint32)
+        if count and k.size:
+            j = np.arange(count, dtype=np.int64)
+            out[:count] = k[np.minimum(k.size - 1, j * stride + stride // 2)]
+        return _t(out)
+
+    def sort_keys(self, keys):
+        return _t(np.sort(_u32(keys)))
 
     def partition(self, keys, vals, splitters):
         k = _u32(keys)
@@ -63,7 +69,17 @@ def _inputs(rank, n, dist_name, pairs):
     gen = zipf_keys if dist_name == "zipf" else uniform_keys
     keys = gen(n + 37 * rank, seed=0x5EED + rank)  # ragged: ranks hold different counts
     if dist_name == "skewed":
-        keys = keys & np.uint32(0x0000FFFF)  # all keys in the lowest top-bits bin
+        keys = keys & np.uint32(0x0000FFFF)  # every key in the lowest 1/65536 of the key range
+    elif dist_name == "hot":
+        keys = keys.copy()
+        keys[: keys.size * 3 // 4] = 0xC0FFEE  # one key holds 3/4 of every rank's keys
+    elif dist_name == "equal":
+        keys = np.full(keys.size, 7, np.uint32)
+    elif dist_name == "maxkey":
+        keys = keys.copy()
+        keys[::2] = 0xFFFFFFFF  # half the keys are the largest key (no bucket above it)
+    elif dist_name == "empty1" and rank == 1:
+        keys = keys[:0]
     vals = (np.arange(keys.size, dtype=np.uint32) + np.uint32(rank << 24)) if pairs else None
     return keys, vals
 
@@ -71,7 +87,7 @@ def _inputs(rank, n, dist_name, pairs):
 def _worker(rank, world, port, n, dist_name, pairs, out_dir, max_message=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if max_message:
-        multi.MAX_MESSAGE = max_message  # exchange in several rounds of pieces
+        multi.MAX_PIECE = max_message  # exchange in several rounds of pieces
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         keys, vals = _inputs(rank, n, dist_name, pairs)
@@ -94,10 +110,12 @@ def _free_port():
                                                                (4, "uniform", True, None), (4, "skewed", False, None),
                                                                (3, "zipf", False, None), (3, "uniform", True, 1000),
                                                                (2, "skewed", False, 777), (8, "uniform", True, 3000),
-                                                               (8, "zipf", False, None)])
+                                                               (8, "zipf", False, None), (4, "hot", True, None),
+                                                               (8, "equal", True, 5000), (3, "maxkey", False, None),
+                                                               (4, "empty1", True, None)])
 def test_dist_sort_gloo(tmp_path, world, dist_name, pairs, max_message):
-    """max_message: pieces per message in the exchange (multi.MAX_MESSAGE, 2^27 keys by default,
-    works around RCCL dropping the second half of >= 2 GiB messages): small values force rounds."""
+    """max_message: keys per exchange message (multi.MAX_PIECE, 2^28 by default: RCCL drops the
+    second half of >= 2 GiB messages): small values force several rounds."""
     n = 50_000
     mp.spawn(_worker, args=(world, _free_port(), n, dist_name, pairs, str(tmp_path), max_message), nprocs=world,
              join=True)
@@ -113,19 +131,32 @@ def test_dist_sort_gloo(tmp_path, world, dist_name, pairs, max_message):
         assert np.array_equal(np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)]), rv)
     else:
         assert np.array_equal(np.concatenate(got), oracle_sort(keys, 8))
-    if dist_name == "uniform":  # splitters (from a 1/16 block sample) balance within a few percent
-        sizes = np.array([g.size for g in got])
-        assert np.abs(sizes - keys.size / world).max() < 0.05 * keys.size
+    sizes = np.array([g.size for g in got])
+    if dist_name in ("uniform", "zipf", "hot", "equal", "maxkey"):
+        # exact-key splitters from the regular sample, hot keys split across ranks: every rank
+        # within 5 % of the mean (duplicate-heavy input no longer piles up)
+        assert np.abs(sizes - keys.size / world).max() < 0.05 * keys.size / world, sizes
 
 
-def test_choose_splitters():
-    h = np.zeros(16, np.int64)
-    h[[1, 5, 9, 13]] = 10
-    s = multi.choose_splitters(h, 4, 4)
-    assert s == [2 << 28, 6 << 28, 10 << 28]
-    # everything in one bin: later splitters saturate and stay monotone
-    h = np.zeros(16, np.int64)
-    h[15] = 100
-    s = multi.choose_splitters(h, 4, 4)
-    assert s == sorted(s) and s[-1] == 0xFFFFFFFF
-    assert multi.choose_splitters(np.ones(4096, np.int64), 1, 12) == []
+def _cap_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys, _ = _inputs(rank, 20_000, "uniform", False)
+        cap = 1000 if rank == 1 else None  # one rank's output is far too small
+        try:
+            multi.dist_sort(_t(keys), 8, ops=NumpyOps(), capacity=cap)
+            res = "ok"
+        except multi.rs.RSortError as e:
+            res = str(e.status)
+        (Path(out_dir) / f"r{rank}").write_text(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_sort_capacity_error_on_every_rank(tmp_path):
+    """a capacity overflow on one rank is reported by EVERY rank, before the
+    exchange, so no rank is left waiting in a collective (the test would hang otherwise)."""
+    world = 3
+    mp.spawn(_cap_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert [(tmp_path / f"r{r}").read_text() for r in range(world)] == ["9"] * world
