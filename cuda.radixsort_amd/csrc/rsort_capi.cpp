@@ -99,6 +99,7 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     const int64_t enough = 2 * (int64_t)(cus > 0 ? cus : 256);
     // partitions: 4096-key tiles (measured at 2^30 keys into 8 ranges: 1024-thread 16384-key
     // tiles need 4-bit bucket digits, i.e. 15 splitter compares per key, and were 1.3x slower)
+    if (k >= 13) return kGeomXL;
     if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
     // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:
@@ -446,7 +447,7 @@ const char *rsort_status_string(int status) {
     switch (status) {
         case RSORT_OK: return "ok";
         case RSORT_ERR_ARG: return "invalid argument";
-        case RSORT_ERR_BITS: return "k_bits outside [1, 12]";
+        case RSORT_ERR_BITS: return "k_bits outside [1, 13]";
         case RSORT_ERR_SIZE: return "n outside [0, 2^32)";
         case RSORT_ERR_ALIGN: return "device buffer not 4-byte aligned";
         case RSORT_ERR_ALLOC: return "allocation failed";

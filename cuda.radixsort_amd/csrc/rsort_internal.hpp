@@ -9,7 +9,7 @@ namespace rsort {
 constexpr int kWave = 64;
 constexpr int kHistThreads = 256;          // workgroup size of the histogram kernel
 constexpr int kMinBits = 1;
-constexpr int kMaxBits = 12;
+constexpr int kMaxBits = 13;            // the reference's SMEM limit (Parallel7.cu:740-745)
 constexpr int kScanThreads = 256;
 constexpr int kScanPerThread = 16;
 constexpr int kScanSegment = kScanThreads * kScanPerThread;  // table entries per scan block
@@ -24,12 +24,15 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 128-B lines
 // (rs_scatter_lines; one workgroup per CU, its LDS holds the tile plus every digit's carry).
 // kGeomLinesPairs (k = 5..8 pairs): 8192-key tiles of 512 threads (keys + values), 64-B lines.
-enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomLinesPairs = 4, kGeomCount = 5 };
+// kGeomXL (k = 13): 4096-key tiles of 128 threads (2 waves), so the 2 x 8192 per-wave counters fit
+// in LDS beside the tile (112 KB keys-only).
+enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomLinesPairs = 4, kGeomXL = 5,
+                  kGeomCount = 6 };
 struct GeomShape {
     int threads;
     int kpt;
 };
-constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {512, 16}};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {512, 16}, {128, 32}};
 // rs_scatter_lines line width. Keys-only stages whole 128-B lines (the L2 line: runs that start or
 // end mid-line cost about a third more HBM time, dev/runlen_lab.hip); pairs keep 64-B lines (two
 // 128-B carry areas do not fit in LDS beside 8192-key tiles of keys and values).
@@ -47,7 +50,9 @@ inline int geom_from_shape(int threads, int tile_keys, int pairs) {
 }
 
 // Internal ranking variants (rs_scatter's RANK template argument).
-enum RankAlgo : int { kRankMatch = 0, kRankSplit = 1, kRankMatchRW = 2, kRankCount = 3, kRankAtomic = 4 };
+// kRankSplit: the reference's 1-bit splits; kRankCount: ballot peer match; kRankAtomic: lane-ordered
+// returning LDS adds (the default where rs_lane_order_probe confirms the lane order).
+enum RankAlgo : int { kRankSplit = 1, kRankCount = 3, kRankAtomic = 4 };
 // Public rsort_rank_algo -> internal variant for the current device (probes lane order once).
 int internal_rank(int public_algo);
 // 1 / 0: same-address ds_add_rtn lanes are served in lane order on the current device; < 0 error.

@@ -33,29 +33,6 @@
 
 #include "rsort_internal.hpp"
 
-// Diagnostic phase stamps (dev/scatter_lab only; compiled out of the library): wave 0 of each
-// workgroup accumulates s_memtime deltas per phase of the scatter tile loop.
-#ifdef RSORT_STAMPS
-#define RS_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
-#define RS_STAMP(i)                                                   \
-    do {                                                              \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-        st_acc[i] += now_ - st_prev;                                  \
-        st_prev = now_;                                               \
-    } while (0)
-#define RS_STAMP_WAIT_LOADS() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#define RS_STAMP_FLUSH()                                                          \
-    do {                                                                          \
-        if (threadIdx.x == 0 && a.stamps)                                         \
-            for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 8 + i_] = st_acc[i_]; \
-    } while (0)
-#else
-#define RS_STAMP_DECL
-#define RS_STAMP(i)
-#define RS_STAMP_WAIT_LOADS()
-#define RS_STAMP_FLUSH()
-#endif
-
 namespace rsort {
 
 
@@ -507,56 +484,31 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
 // (position - first position of the digit in the tile) -- the firstIndices rank formula of
 // P7:293-294 with the running offset kept in registers.
 //
-// The next tile's keys are loaded into registers as soon as the current tile is staged in
-// LDS, so its HBM reads overlap the current tile's global writes.
-//
-// Template knobs (the library picks one configuration per (BITS, PAIRS); dev/scatter_lab
-// times the others):
-//   RANK  kRankMatch   leader lane bumps the per-wave digit counter with a returning ds_add,
-//                      the base is broadcast with ds_bpermute (slots never wait on each other)
-//         kRankMatchRW all lanes read the counter, the leader writes it back (no broadcast;
-//                      one LDS round trip per slot on the wave's critical path)
-//         kRankCount   count first (one non-returning ds_add per key), scan the per-wave
-//                      counters into final tile positions, then peer-match each slot and write
-//                      the key straight to its LDS position: no per-key rank registers and no
-//                      separate staging loop (lowest VGPR use -> most workgroups per CU)
+// This is the general pass (any k, unaligned outputs, local-only mode, the reference's 1-bit
+// split ranking); the k = 3..8 sorts with 16-B aligned buffers run rs_scatter_lines below.
+//   RANK  kRankAtomic  count first (per-wave LDS digit counters), scan them into tile positions,
+//                      then one returning LDS add per key: the lane-ordered add IS the key's
+//                      stable position (rank_add)
+//         kRankCount   the same with the wave64 ballot peer match instead of the lane order
 //         kRankSplit   k stable 1-bit splits (the reference's algorithm)
-//   DEST  stage each key's global destination next to it in LDS (keys only): the output
-//         phase then reads (key, destination) with two conflict-free reads, no dependent lookup
 //   MINW  minimum waves per SIMD requested from the register allocator (0 = compiler's choice)
-//   ABL   ablation bits for dev/scatter_lab only (1 = skip ranking, 2 = skip global stores)
-template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW = 0,
-          bool DEST = false, int ABL = 0, int WCG = 0>
+template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW = 0>
 __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(ScatterArgs a) {
-    constexpr bool WC = WCG > 0;
-    static_assert(!(DEST && PAIRS), "DEST staging is for keys-only sorts");
     constexpr bool COUNT_FIRST = (RANK == kRankCount || RANK == kRankAtomic);
-    static_assert(!WC || (COUNT_FIRST && (1u << BITS) <= (uint32_t)THREADS && (WCG == 16 || WCG == 32)),
-                  "write-combining needs the count-first ranking and one digit per thread");
+    static_assert(COUNT_FIRST || RANK == kRankSplit, "ranking variant");
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;            // tile positions per wave
     constexpr uint32_t T = THREADS * KPT;       // tile keys
     constexpr int DPT = (R > THREADS) ? (int)(R / THREADS) : 1;  // digits owned per thread
-    constexpr bool MATCH = (RANK == kRankMatch || RANK == kRankMatchRW);
-    static_assert(!COUNT_FIRST || !DEST, "count-first ranking writes keys during ranking");
-    constexpr uint32_t NCNT = (MATCH || COUNT_FIRST) ? W * R : R;
+    constexpr uint32_t NCNT = COUNT_FIRST ? W * R : R;
 
     __shared__ uint32_t s_keys[T];
     __shared__ uint32_t s_vals[PAIRS ? T : 1];
-    __shared__ uint32_t s_dest[DEST ? T : 1];
     __shared__ uint16_t s_aux[RANK == kRankSplit ? T : 1];
     __shared__ uint32_t s_cnt[NCNT];
-    __shared__ uint32_t s_delta[WC ? 1 : R];
+    __shared__ uint32_t s_delta[R];
     __shared__ uint32_t s_ws[W];
-    // write-combining state (WC): each digit's carry -- the < WCG keys past its last whole
-    // line, held back until the next tile completes that line -- and per tile: {delta, lim}
-    // (run key at LDS i goes to delta + i if i < lim, else to carry slot i - lim) and
-    // {A, f} (carry slots q < f are flushed to A + q this tile)
-    __shared__ uint32_t s_carry[WC ? R * WCG : 1];
-    __shared__ uint32_t s_cvals[WC && PAIRS ? R * WCG : 1];
-    __shared__ uint2 s_info[WC ? R : 1];
-    __shared__ uint2 s_flush[WC ? R : 1];
 
     const uint32_t t = threadIdx.x;
     const uint32_t w = t / kWave;
@@ -605,27 +557,21 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
-    uint32_t wc_c = 0;  // WC: carry count of digit t (the chunk's first line is written partial)
 
-    RS_STAMP_DECL
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        // output slot j of thread t (LDS position t + j*THREADS) is real iff j*THREADS < olim;
-        // comparing constants against one register keeps LICM from hoisting KPT positions
         // tl: the thread index made opaque per tile, so LICM cannot hoist the KPT output
-        // positions tl + j*THREADS out of the loop into KPT live registers
+        // positions tl + j*THREADS out of the loop into KPT live registers; output slot j of
+        // thread t (LDS position t + j*THREADS) is real iff j*THREADS < olim
         uint32_t tl = t;
         asm volatile("" : "+v"(tl));
         const uint32_t olim = valid > tl ? valid - tl : 0u;
         const uint64_t nb = tb + T;
-        RS_STAMP_WAIT_LOADS();
-        RS_STAMP(0);  // waiting for this tile's keys (and the previous tile's stores)
 
         if constexpr (!COUNT_FIRST) {
             for (uint32_t i = t; i < NCNT; i += THREADS) s_cnt[i] = 0;
             __syncthreads();
         }
-        RS_STAMP(1);  // counter reset + barrier
 
         if constexpr (COUNT_FIRST) {
             // ---- 0. each wave clears its own counters: no other wave touches s_cnt[w][*]
@@ -636,198 +582,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 #pragma unroll
             for (int j = 0; j < KPT; ++j) count_add(&s_cnt[w * R], dig(key[j]));
             __syncthreads();
-            RS_STAMP(2);  // histogram
             // ---- 2. digit scan: s_cnt[w][d] <- tile position of wave w's first key of digit d
-            uint32_t tot[DPT];
-            uint32_t mine = 0;
-#pragma unroll
-            for (int i = 0; i < DPT; ++i) {
-                const uint32_t d = t * DPT + i;
-                uint32_t acc = 0;
-                if (d < R) {
-#pragma unroll
-                    for (int v = 0; v < W; ++v) {
-                        const uint32_t x = s_cnt[v * R + d];
-                        s_cnt[v * R + d] = acc;
-                        acc += x;
-                    }
-                }
-                tot[i] = acc;
-                mine += acc;
-            }
-            uint32_t all;
-            uint32_t start = block_excl_scan<THREADS>(mine, s_ws, all);
-            const bool last_tile = nb >= cend;
-#pragma unroll
-            for (int i = 0; i < DPT; ++i) {
-                const uint32_t d = t * DPT + i;
-                if (d < R) {
-#pragma unroll
-                    for (int v = 0; v < W; ++v) s_cnt[v * R + d] += start;
-                    if constexpr (WC) {
-                        // pending output of digit d = its carry (c keys from A = g - c) followed
-                        // by this tile's run; write up to the last whole line (all of it on the
-                        // chunk's last tile), carry the rest. When anything is written, the
-                        // whole old carry is (it lies below the first line end past A).
-                        uint32_t leff = tot[i];  // padding (last tile only) ends the largest digit's run
-                        if (valid < T && d == dig(0xFFFFFFFFu)) leff -= T - valid;
-                        const uint32_t g = run[i], c = wc_c, A = g - c, e = g + leff;
-                        const uint32_t fe = e & ~(uint32_t)(WCG - 1);
-                        const uint32_t Wend = last_tile ? e : (fe > A ? fe : A);
-                        s_info[d] = make_uint2(g - start, start + (Wend - g));  // lim may wrap below start
-                        s_flush[d] = make_uint2(A, Wend > A ? c : 0u);
-                        wc_c = e - Wend;
-                        run[i] = e;
-                    } else {
-                        s_delta[d] = run[i] - start;
-                        run[i] += tot[i];
-                    }
-                }
-                start += tot[i];
-            }
-            __syncthreads();
-            RS_STAMP(3);  // barrier + digit scan
-            if constexpr (WC) {
-                // ---- 2b. flush the old carries that complete a line this tile
-                if (!a.local_only) {
-#pragma unroll 4
-                    for (uint32_t item = tl; item < R * WCG; item += THREADS) {
-                        const uint2 fl = s_flush[item / WCG];
-                        const uint32_t q = item % WCG;
-                        if (q < fl.y) {
-                            a.kout[fl.x + q] = s_carry[item];
-                            if constexpr (PAIRS) a.vout[fl.x + q] = s_cvals[item];
-                        }
-                    }
-                }
-            }
-            // ---- 3. rank each slot; the counter IS the destination: write the key now
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                // recompute the digit: CSE with the histogram step would keep KPT addresses alive
-                asm volatile("" : "+v"(key[j]));
-                const uint32_t d = dig(key[j]);
-                if constexpr (RANK == kRankAtomic) {
-                    // one returning LDS add per key: gfx950 serves the lanes of a ds_add_rtn_u32
-                    // that hit the same address in ascending lane order, so lane l receives
-                    // base + (#lower lanes with its digit) -- the stable rank, with no ballots.
-                    // (verified on every digit width / layout: dev/lds_order_lab.hip; the
-                    // library re-checks it per device before selecting this path)
-                    const uint32_t p = rank_add(&s_cnt[w * R], d);
-                    s_keys[p] = key[j];
-                    if constexpr (PAIRS) s_vals[p] = val[j];
-                    continue;
-                }
-                uint32_t mlo, mhi;
-                peer_mask<BITS>(d, mlo, mhi);
-                const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
-                const uint32_t old = s_cnt[w * R + d];
-                if (pre == 0) s_cnt[w * R + d] = old + (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi));
-                s_keys[old + pre] = key[j];
-                if constexpr (PAIRS) s_vals[old + pre] = val[j];
-            }
-            __syncthreads();
-            RS_STAMP(4);  // ranking + staging + barrier
-            if (nb < cend) load_tile(nb, key, val);
-            if (a.local_only) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = tl + j * THREADS;
-                    if ((uint32_t)(j * THREADS) < olim) {
-                        a.kout[tb + i] = s_keys[i];
-                        if constexpr (PAIRS) a.vout[tb + i] = s_vals[i];
-                    }
-                }
-            } else if constexpr (WC) {
-                // ---- 4. run keys below lim complete lines: store; the rest become the carry
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = tl + j * THREADS;
-                    if (valid == T || (uint32_t)(j * THREADS) < olim) {
-                        const uint32_t k = s_keys[i];
-                        const uint32_t d = dig(k);
-                        const uint2 info = s_info[d];
-                        if ((int)(i - info.y) < 0) {
-                            if constexpr ((ABL & 2) != 0) {
-                                asm volatile("" ::"v"(k), "v"(info.x));
-                                continue;
-                            }
-                            a.kout[info.x + i] = k;
-                            if constexpr (PAIRS) a.vout[info.x + i] = s_vals[i];
-                        } else {
-                            s_carry[d * WCG + (i - info.y)] = k;
-                            if constexpr (PAIRS) s_cvals[d * WCG + (i - info.y)] = s_vals[i];
-                        }
-                    }
-                    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-                }
-            } else {
-                const bool full = valid == T;
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = tl + j * THREADS;
-                    if (full || (uint32_t)(j * THREADS) < olim) {
-                        const uint32_t k = s_keys[i];
-                        const uint32_t pos = s_delta[dig(k)] + i;
-                        if constexpr ((ABL & 2) != 0) {
-                            asm volatile("" ::"v"(k), "v"(pos));
-                            continue;
-                        }
-                        a.kout[pos] = k;
-                        if constexpr (PAIRS) a.vout[pos] = s_vals[i];
-                    }
-                    // issue the output in groups of 8 keys: bounds the LDS reads in flight
-                    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            RS_STAMP(5);  // output: LDS reads + global stores issued
-        } else if constexpr (MATCH) {
-            // ---- wave peer-match ranking; counters s_cnt[w][digit]. Per slot: the mask of
-            // lanes holding the same digit (BITS ballots, 4 VALU per bit), the rank among them
-            // (mbcnt), and the per-wave digit counter bumped once per digit group.
-            uint32_t rk[KPT];    // rank of the key inside its wave (counter base + rank in group)
-            uint32_t info[KPT];  // digit | (kRankMatch: rank in group << 16 | leader lane << 24)
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t d = dig(key[j]);  // padding 0xFFFFFFFF -> the largest digit
-                if constexpr ((ABL & 1) != 0) {
-                    rk[j] = (uint32_t)j * kWave + lane;
-                    info[j] = d;
-                    continue;
-                }
-                uint32_t mlo, mhi;
-                peer_mask<BITS>(d, mlo, mhi);
-                const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
-                const uint32_t cnt = (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi));
-                if constexpr (RANK == kRankMatch) {
-                    // returning ds_add by the group's lowest lane; broadcast in the second loop
-                    const uint32_t leader = mlo ? (uint32_t)__builtin_ctz(mlo) : 32u + (uint32_t)__builtin_ctz(mhi);
-                    rk[j] = 0;
-                    if (pre == 0) rk[j] = atomicAdd(&s_cnt[w * R + d], cnt);
-                    info[j] = d | (pre << 16) | (leader << 24);
-                    // Materialise the packed state now: otherwise the compiler sinks the leader
-                    // computation to its use and keeps all KPT 64-bit masks alive (~+40 VGPRs).
-                    asm volatile("" : "+v"(info[j]));
-                } else {
-                    // every lane reads the counter (same address within a group: broadcast), the
-                    // group's lowest lane writes it back; in-order LDS keeps slots consistent
-                    const uint32_t old = s_cnt[w * R + d];
-                    if (pre == 0) s_cnt[w * R + d] = old + cnt;
-                    rk[j] = (old + pre) | (d << 16);  // wave rank < 64*KPT, digit < 2^12: one register
-                    asm volatile("" : "+v"(rk[j]));   // materialise now (else old/pre/d stay live per slot)
-                    info[j] = 0;
-                }
-                __builtin_amdgcn_sched_barrier(0);  // bound live ranges: one slot's temporaries at a time
-            }
-            if constexpr (RANK == kRankMatch && (ABL & 1) == 0) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j)
-                    rk[j] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((info[j] >> 24) << 2), (int)rk[j]) +
-                            ((info[j] >> 16) & 0xFFu);
-            }
-            RS_STAMP(2);  // ranking
-            __syncthreads();
-            // ---- digit scan: per owned digit, exclusive over waves; block scan over digits
             uint32_t tot[DPT];
             uint32_t mine = 0;
 #pragma unroll
@@ -859,27 +614,32 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                 start += tot[i];
             }
             __syncthreads();
-            RS_STAMP(3);  // barrier + digit scan
-            // ---- stage the tile in digit order (and, with DEST, each key's global position)
+            // ---- 3. rank each slot; the counter IS the destination: write the key now
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                uint32_t d, r;
-                if constexpr (RANK == kRankMatchRW && (ABL & 1) == 0) {
-                    d = rk[j] >> 16;
-                    r = rk[j] & 0xFFFFu;
-                } else {
-                    d = info[j] & 0xFFFFu;
-                    r = rk[j];
+                // recompute the digit: CSE with the histogram step would keep KPT addresses alive
+                asm volatile("" : "+v"(key[j]));
+                const uint32_t d = dig(key[j]);
+                if constexpr (RANK == kRankAtomic) {
+                    // one returning LDS add per key: gfx950 serves the lanes of a ds_add_rtn_u32
+                    // that hit the same address in ascending lane order, so lane l receives
+                    // base + (#lower lanes with its digit) -- the stable rank, with no ballots
+                    // (rank_add; the library probes this once per device, rs_lane_order_probe)
+                    const uint32_t p = rank_add(&s_cnt[w * R], d);
+                    s_keys[p] = key[j];
+                    if constexpr (PAIRS) s_vals[p] = val[j];
+                    continue;
                 }
-                const uint32_t pos = s_cnt[w * R + d] + r;
-                s_keys[pos] = key[j];
-                if constexpr (PAIRS) s_vals[pos] = val[j];
-                if constexpr (DEST) s_dest[pos] = s_delta[d] + pos;
+                uint32_t mlo, mhi;
+                peer_mask<BITS>(d, mlo, mhi);
+                const uint32_t pre = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                const uint32_t old = s_cnt[w * R + d];
+                if (pre == 0) s_cnt[w * R + d] = old + (uint32_t)(__builtin_popcount(mlo) + __builtin_popcount(mhi));
+                s_keys[old + pre] = key[j];
+                if constexpr (PAIRS) s_vals[old + pre] = val[j];
             }
             __syncthreads();
-            RS_STAMP(4);  // staging + barrier
             if (nb < cend) load_tile(nb, key, val);
-            // ---- write each digit's run: consecutive threads -> consecutive addresses
             if (a.local_only) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
@@ -896,21 +656,14 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                     const uint32_t i = tl + j * THREADS;
                     if (full || (uint32_t)(j * THREADS) < olim) {
                         const uint32_t k = s_keys[i];
-                        uint32_t pos;
-                        if constexpr (DEST) pos = s_dest[i];
-                        else pos = s_delta[dig(k)] + i;
-                        if constexpr ((ABL & 2) != 0) {
-                            asm volatile("" ::"v"(k), "v"(pos));
-                            continue;
-                        }
-                        // ranks are fake under ABL & 1: keep the ablation's stores inside the buffer
-                        if constexpr ((ABL & 1) != 0) pos = (uint32_t)((uint64_t)pos % a.n);
+                        const uint32_t pos = s_delta[dig(k)] + i;
                         a.kout[pos] = k;
                         if constexpr (PAIRS) a.vout[pos] = s_vals[i];
                     }
+                    // issue the output in groups of 8 keys: bounds the LDS reads in flight
+                    if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
                 }
             }
-            RS_STAMP(5);  // output: LDS reads + global stores issued
         } else {
             // ---- RANK_SPLIT: k stable 1-bit splits in LDS (reference P5:89-146 / P7:79-191)
             uint32_t dg[KPT];
@@ -991,7 +744,6 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             if (nb < cend) load_tile(nb, key, val);
         }
     }
-    RS_STAMP_FLUSH();
 }
 
 // ------------------------------------------------------------------------------ small kernels
@@ -1019,7 +771,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, bool RF = true, int ABL = 0, int NT = 0>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -1038,7 +790,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];  // + padding sink
     __shared__ __attribute__((aligned(16))) uint32_t s_vstage[PAIRS ? CAP + R * G + 4 : 4];
     __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
-    __shared__ uint32_t s_lim[RF ? 1 : R];  // !RF: per digit, the LDS index past its last whole line
     __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
@@ -1116,10 +867,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         const uint64_t gp = (uint64_t)(info.x + L * G + q);
         u32x4 vv;
         if constexpr (PAIRS) vv = *reinterpret_cast<const u32x4 *>(&s_vstage[L * G + q]);
-        if constexpr ((ABL & 2) != 0) {  // dev/scatter_lab ablation: no global stores
-            asm volatile("" ::"v"(kv), "v"(gp));
-            return;
-        }
         if (lo <= q) {
             if constexpr ((NT & 2) != 0) {  // non-temporal whole-line stores (dev/scatter_lab experiment)
                 __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
@@ -1143,7 +890,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
 
-    RS_STAMP_DECL
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
         const bool full = valid == T && head == 0;
@@ -1153,14 +899,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         // ... and, in slot 0, iff this lane's tile position is not before the chunk (head)
         const bool h0 = base >= head;
         head = 0;
-        RS_STAMP_WAIT_LOADS();
-        RS_STAMP(0);
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
         for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
-        // RF (rank first): the returning add IS the key's rank among its wave's keys of that digit
+        // rank first: the returning add IS the key's rank among its wave's keys of that digit
         // (lane order, kRankAtomic); two ranks (< 2^16) per register
-        uint32_t rk[RF ? (KPT + 1) / 2 : 1];
+        uint32_t rk[(KPT + 1) / 2];
         // split digits (a compare per splitter) are kept from step 1, 4 bits each, for step 3
         constexpr bool PD = DMODE == kDigitSplit && BITS <= 4;
         uint32_t dpk[PD ? (KPT + 7) / 8 : 1];
@@ -1171,19 +915,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                if constexpr (RF) {
-                    // (ABL & 4: dev/scatter_lab ablation -- plain lane-ordered adds, no aggregation;
-                    // measured: aggregation is ~2% faster even on uniform keys, 1.7x on clustered)
-                    const uint32_t dj = dig(key[j]);
-                    if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                    const uint32_t r = (ABL & 4) ? atomicAdd(&s_cnt[w * R + dj], 1u)
-                                                 : rank_add(&s_cnt[w * R], dj);
-                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
-                } else {
-                    const uint32_t dj = dig(key[j]);
-                    if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                    count_add(&s_cnt[w * R], dj);
-                }
+                // (measured: rank_add's aggregation is ~2% faster than plain lane-ordered adds even
+                // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
+                const uint32_t dj = dig(key[j]);
+                if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
+                const uint32_t r = rank_add(&s_cnt[w * R], dj);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
 #pragma unroll
@@ -1192,13 +929,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 if constexpr (PD) dpk[j / 8] |= d << (4 * (j % 8));
                 uint32_t r = 0;
                 if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
-                if constexpr (RF) rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         }
         // next tile's keys: in flight through the scan, staging and output phases
         if (nb < cend) load_tile(nb, nkey, nval);
         __syncthreads();
-        RS_STAMP(2);
 
         // ---- 2. segments, line records, carry copy, counter bases
         // the group's TPD threads split the W per-wave counters of digit d; the leader combines
@@ -1218,7 +954,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         uint32_t gpre, cnt;
         group_scan<TPD>(part, sub, gpre, cnt);
         uint32_t wcnt = 0, A = 0, e = 0;
-        RS_STAMP(1);
         if (leader) {
             A = g_run - carry;  // line-aligned
             e = g_run + cnt;
@@ -1226,7 +961,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         }
         uint32_t nseg;
         const uint32_t S = block_excl_scan1<THREADS>(wcnt, s_ws, nseg);  // next s_ws write is a tile later
-        RS_STAMP(3);
         const uint32_t gS = group_lane<TPD>(S, 0), gw = group_lane<TPD>(wcnt, 0);
         const uint32_t gA = group_lane<TPD>(A, 0), gc = group_lane<TPD>(carry, 0), ginv = group_lane<TPD>(inv, 0);
         {
@@ -1238,10 +972,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 for (uint32_t i = 0; i < WPT; ++i) {
                     const uint32_t v = sub * WPT + i;
                     if (v < (uint32_t)W) {
-                        // RF: {LDS base | the digit's line limit << 16} (both < CAP < 2^16), read
-                        // back with one ds_read_b32 per key in step 3
-                        if constexpr (RF) s_cnt[v * R + d] = acc | ((gS + gw) << 16);
-                        else s_cnt[v * R + d] = acc;
+                        // {LDS base | the digit's line limit << 16} (both < CAP < 2^16), read back
+                        // with one ds_read_b32 per key in step 3
+                        s_cnt[v * R + d] = acc | ((gS + gw) << 16);
                     }
                     acc += wx[i];
                 }
@@ -1298,16 +1031,13 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
             if (leader) {
                 s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
-                if constexpr (!RF) s_lim[d] = gS + gw;
                 if (gw > 0) inv = 0;
                 carry = e - (A + gw);  // pending - written
                 g_run = e;
                 if (nb >= cend) s_flush[d] = make_uint2(g_run - carry, inv | (carry << 8));
             }
         }
-        RS_STAMP(4);
         __syncthreads();
-        RS_STAMP(5);
 
         // ---- 3. rank (lane-ordered returning LDS add) and stage; tails go to the carry.
         // Batches of 8 slots: all atomics and limit reads are issued before the first store,
@@ -1323,16 +1053,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
                 if constexpr (PD) dd[u] = (dpk[j / 8] >> (4 * (j % 8))) & 15u;
                 else dd[u] = dig(key[j]);
-                if constexpr (RF) {
-                    const uint32_t bl = s_cnt[w * R + dd[u]];
-                    pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
-                    ll[u] = bl >> 16;
-                } else {
-                    // padding slots (the grid's last tile only) count into a scratch counter
-                    const uint32_t ci = (full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0))) ? w * R + dd[u] : W * R;
-                    pp[u] = atomicAdd(&s_cnt[ci], 1u);
-                    ll[u] = s_lim[dd[u]];
-                }
+                const uint32_t bl = s_cnt[w * R + dd[u]];
+                pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+                ll[u] = bl >> 16;
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1345,13 +1068,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
         }
         __syncthreads();
-        RS_STAMP(6);
 
         // ---- 4. whole lines out: 4 keys per lane (16-B aligned in LDS and in global memory)
         const uint32_t nq = (nseg / G) * QPL;
 #pragma unroll 2
         for (uint32_t item = t; item < nq; item += THREADS) out_quad(item);
-        RS_STAMP(7);
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             key[j] = nkey[j];
@@ -1369,7 +1090,6 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             }
         }
     }
-    RS_STAMP_FLUSH();
 }
 
 // Top-bits histogram of every stride-th 256-key block (the multi-GPU sort's splitter sample):
@@ -1547,7 +1267,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
                 constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
                 if (geom == kGeomSmall && rank == kRankAtomic && aligned16)
                     return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
-                                                                      PAIRS, kDigitSplit, true, 0, PAIRS ? 2 : 3>);
+                                                                      PAIRS, kDigitSplit, PAIRS ? 2 : 3>);
             }
             if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
         }
@@ -1563,7 +1283,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
             // aligned outputs, like kGeomLines)
             constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
             if (rank == kRankAtomic && aligned16)
-                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, true, 0, 3>);
+                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, 3>);
         }
         return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
     }
@@ -1577,7 +1297,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
             if (rank == kRankAtomic && aligned16)
                 return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
                                                                   PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
-                                                                  kDigitShift, true, 0, PAIRS ? 2 : 3>);
+                                                                  kDigitShift, PAIRS ? 2 : 3>);
             return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }
@@ -1587,9 +1307,19 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
     return nullptr;
 }
 
+// k = 13 (the reference's largest digit, Parallel7.cu:740-745): 128-thread 4096-key tiles, every ranking
+template <bool PAIRS>
+static void *scatter_pick13(int rank, int dmode, int geom) {
+    if (dmode != kDigitShift || geom != kGeomXL) return nullptr;
+    if (rank == kRankSplit) return scatter_fn<13, PAIRS, kRankSplit, kDigitShift, kGeomXL>();
+    if (rank != kRankAtomic && rank != kRankCount) return nullptr;
+    return scatter_cf<13, PAIRS, kDigitShift, kGeomXL>(rank);
+}
+
 template <int BITS>
 static void *scatter_pick(int pairs, int rank, int dmode, int geom, int aligned16) {
-    return pairs ? scatter_pick2<BITS, true>(rank, dmode, geom, aligned16)
+    if constexpr (BITS == 13) return pairs ? scatter_pick13<true>(rank, dmode, geom) : scatter_pick13<false>(rank, dmode, geom);
+    else return pairs ? scatter_pick2<BITS, true>(rank, dmode, geom, aligned16)
                  : scatter_pick2<BITS, false>(rank, dmode, geom, aligned16);
 }
 
@@ -1607,6 +1337,7 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
         case 10: return scatter_pick<10>(pairs, rank, dmode, geom, aligned16);
         case 11: return scatter_pick<11>(pairs, rank, dmode, geom, aligned16);
         case 12: return scatter_pick<12>(pairs, rank, dmode, geom, aligned16);
+        case 13: return scatter_pick<13>(pairs, rank, dmode, geom, aligned16);
         default: return nullptr;
     }
 }
@@ -1614,32 +1345,55 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
 #endif  // RSORT_LAB_LITE
 
 // ------------------------------------------------------------------------------ lane-order probe
-// Every lane of a wave adds to one of a few LDS counters with a returning atomic and checks the
-// value against the lane-ordered expectation (old + #lower lanes with the same counter).
-__global__ __launch_bounds__(256) void rs_lane_order_probe(uint32_t *bad) {
-    __shared__ uint32_t cnt[4 * 256];
+// The default ranking (kRankAtomic) rests on gfx950's LDS serving the lanes of one ds_add_rtn_u32
+// that hit the same address in ascending lane order. The probe replays the production conditions
+// of rs_scatter_lines<8, 1024, 16, ...>: 1024-thread workgroups, the same per-wave rows of 256
+// counters, the SAME device function (rank_add, with its aggregated path for >= 16 equal lanes),
+// digit ranges 1..256 and runs of equal digits (the clustered input that takes the aggregated path),
+// partial exec masks -- and checks every returned rank against old value + #lower active lanes
+// with the same digit (a register-only count). Any mismatch makes the library use ballots.
+__global__ __launch_bounds__(1024) void rs_lane_order_probe(uint32_t *bad) {
+    constexpr uint32_t R = 256;
+    constexpr int W = 1024 / kWave;
+    __shared__ uint32_t s_cnt[W * R];
     const uint32_t t = threadIdx.x, w = t / kWave, lane = lane_id();
-    for (uint32_t i = t; i < 4 * 256; i += 256) cnt[i] = 0;
+    for (uint32_t i = t; i < W * R; i += 1024) s_cnt[i] = 0;
     __syncthreads();
     uint32_t nbad = 0;
-    for (uint32_t it = 0; it < 64; ++it) {
+    for (uint32_t it = 0; it < 96; ++it) {
         uint32_t h = (blockIdx.x * 0x9E3779B9u) ^ (it * 0x85EBCA6Bu) ^ (t * 0xC2B2AE35u);
         h ^= h >> 16;
         h *= 0x7feb352dU;
         h ^= h >> 15;
-        const uint32_t range = (it & 3) == 0 ? 1u : (it & 3) == 1 ? 3u : (it & 3) == 2 ? 16u : 256u;
-        const uint32_t d = h % range;
-        const uint32_t idx = w * 256 + d;
-        const uint32_t before = cnt[idx];
+        const uint32_t hw = __builtin_amdgcn_readfirstlane((blockIdx.x * 0x27D4EB2Fu) ^ (it * 0x165667B1u) ^ w);
+        uint32_t d;
+        switch (it % 6) {
+            case 0: d = 0; break;                                     // one counter
+            case 1: d = h % 3; break;
+            case 2: d = h % 16; break;
+            case 3: d = h % 256; break;                               // uniform keys
+            case 4: d = (hw + lane / (1u + hw % 37)) % 256; break;    // runs of equal digits
+            default: d = (lane < (hw % 64) ? hw : hw + 1 + (h & 1)) % 256;  // a run crossing the slot
+        }
+        // every third iteration all lanes take part; else a hashed subset (partial exec mask)
+        const bool active = (it % 3 == 0) || ((h >> 7) % 4 != 0);
+        const uint32_t before = s_cnt[w * R + d];
         uint32_t below = 0;
         for (int l = 0; l < kWave; ++l) {
             const uint32_t dl = __shfl(d, l);  // every lane takes part (bpermute reads active lanes only)
-            below += ((uint32_t)l < lane && dl == d) ? 1u : 0u;
+            const uint32_t al = __shfl(active ? 1u : 0u, l);
+            below += ((uint32_t)l < lane && al && dl == d) ? 1u : 0u;
         }
         __builtin_amdgcn_wave_barrier();
-        const uint32_t got = atomicAdd(&cnt[idx], 1u);
-        nbad += got != before + below;
+        if (active) {
+            const uint32_t got = rank_add(&s_cnt[w * R], d);
+            nbad += got != before + below;
+        }
         __builtin_amdgcn_wave_barrier();
+        if (it % 24 == 23) {  // keep the counters small (each wave clears its own row)
+            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+            __builtin_amdgcn_wave_barrier();
+        }
     }
     if (nbad) atomicAdd(bad, nbad);
 }
@@ -1657,7 +1411,7 @@ int lane_order_probe() {
     bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&bad, 4) == hipSuccess && hipMemsetAsync(bad, 0, 4, s) == hipSuccess;
     if (ok) {
-        rs_lane_order_probe<<<512, 256, 0, s>>>(bad);
+        rs_lane_order_probe<<<512, 1024, 0, s>>>(bad);
         ok = hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(&host, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -1689,6 +1443,7 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
         case 10: return hist_bits<10>(dmode, a, s);
         case 11: return hist_bits<11>(dmode, a, s);
         case 12: return hist_bits<12>(dmode, a, s);
+        case 13: return hist_bits<13>(dmode, a, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1704,14 +1459,15 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     if (geom < 0 || geom >= kGeomCount) return hipErrorInvalidValue;
     void *fn = scatter_kernel(bits, pairs, rank_algo, dmode, geom, aligned16);
     if (!fn) return hipErrorInvalidValue;
-    // k = 3, 4 keys of up to 2^27 (whose ping-pong buffers fit the 256-MiB Infinity Cache together):
-    // default-policy stores, so the next pass reads them from the cache (dev/scatter_lab LAB_K4,
+    // k = 3, 4 keys of up to 2^26 (the size measured): default-policy stores. A pass writes 256 MiB
+    // there, as much as the Infinity Cache holds (the two ping-pong buffers, 512 MiB, do NOT fit
+    // together), so part of what the next pass reads is still on die (dev/scatter_lab LAB_K4,
     // 2^26 keys: 0.105 ms per pass against 0.113 with non-temporal stores; 2^30: 1.81 vs 1.75)
-    if (a.n <= ((uint64_t)1 << 27) && !pairs && dmode == kDigitShift && geom == kGeomSmall &&
+    if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomSmall &&
         rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
         constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
-        fn = bits == 3 ? reinterpret_cast<void *>(&rs_scatter_lines<3, TH, KP, kLineKeys, false, kDigitShift, true, 0, 1>)
-                       : reinterpret_cast<void *>(&rs_scatter_lines<4, TH, KP, kLineKeys, false, kDigitShift, true, 0, 1>);
+        fn = bits == 3 ? reinterpret_cast<void *>(&rs_scatter_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>)
+                       : reinterpret_cast<void *>(&rs_scatter_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>);
     }
     ScatterArgs copy = a;
     void *args[] = {&copy};

@@ -73,19 +73,17 @@ static const char *g_filter = nullptr;
 template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
 void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift = 0, int reps = 5);
 
-template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int MINW, bool DEST = false, int ABL = 0,
-          int WCG = 0>
+template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int MINW>
 void variant(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
-    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
-                                          rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, kDigitShift, MINW, DEST, ABL, WCG>,
+    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult, rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, kDigitShift, MINW>,
                                           shift, reps);
 }
 
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, bool RF = true, int ABL = 0, int NT = 0>
+// NT: 1 non-temporal loads, 2 non-temporal stores (rs_scatter_lines)
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int NT = 0>
 void lines(Ctx &c, const char *name, double wave_mult, int shift = 0, int reps = 5) {
-    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult,
-                                          rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, RF, ABL, NT>, shift,
-                                          reps);
+    run_variant<BITS, THREADS, KPT, PAIRS>(c, name, wave_mult, rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, kDigitShift, NT>,
+                                          shift, reps);
 }
 
 template <int BITS, int THREADS, int KPT, bool PAIRS, typename K>
@@ -140,33 +138,6 @@ void run_variant(Ctx &c, const char *name, double wave_mult, K kern, int shift, 
     const double bytes = (PAIRS ? 16.0 : 8.0) * c.n;
     printf("%-34s bpc=%d tpc=%-5llu chunks=%-6llu %8.3f ms  %7.1f GB/s  %5.1f%%  mismatch=%llu\n", name, bpc,
            (unsigned long long)tpc, (unsigned long long)chunks, ms, bytes / ms / 1e6, bytes / ms / 1e6 / 80.0, bad);
-#ifdef RSORT_STAMPS
-    {
-        std::vector<unsigned long long> st(chunks * 8);
-        CK(hipMemcpy(st.data(), c.stamps, chunks * 8 * 8, hipMemcpyDeviceToHost));
-        double sum[8] = {0}, tot = 0;
-        for (uint64_t b = 0; b < chunks; ++b)
-            for (int i = 0; i < 8; ++i) sum[i] += st[b * 8 + i];
-        for (int i = 0; i < 8; ++i) tot += sum[i];
-        const char *names[8] = {"wait-keys", "2a:cnt-reads", "1:rank+bar", "2b:scan", "2c:bases+carry", "2d:bar", "3:stage+bar", "4:output"};
-        printf("    stamps per tile (cycles, wave 0):");
-        for (int i = 0; i < 8; ++i) printf(" %s=%.0f (%.0f%%)", names[i], sum[i] / chunks / tpc, 100.0 * sum[i] / tot);
-        printf("\n");
-        // per-chunk totals: the slowest workgroup sets the kernel time
-        double mn = 1e30, mx = 0;
-        uint64_t bmx = 0;
-        for (uint64_t b = 0; b < chunks; ++b) {
-            double tb = 0;
-            for (int i = 0; i < 8; ++i) tb += st[b * 8 + i];
-            if (tb < mn) mn = tb;
-            if (tb > mx) { mx = tb; bmx = b; }
-        }
-        printf("    per-chunk cycles: min=%.0f avg=%.0f max=%.0f (chunk %llu:", mn, tot / chunks, mx,
-               (unsigned long long)bmx);
-        for (int i = 0; i < 8; ++i) printf(" %.0f", (double)st[bmx * 8 + i] / tpc);
-        printf(" per tile)\n");
-    }
-#endif
     fflush(stdout);
 }
 
@@ -240,128 +211,73 @@ int main(int argc, char **argv) {
         printf("copy dwordx4 (32/CU) %8.3f ms %7.1f GB/s\n", ms4b, 8.0 * c.n / ms4b / 1e6);
     }
 #ifdef LINES_ONLY
-    // -DLINES_ONLY: just the line-combining kernels (fast rebuilds while tuning them)
+    // -DLINES_ONLY: just the line-combining kernels (fast rebuilds); phase stamps of the line kernel
+    // live in dev/lines_exp.hip (-DLX_STAMPS)
     if (getenv("LAB_K4")) {
         variant<4, 512, 16, false, kRankAtomic, 4>(c, "k4 512x16 atomic w4 (lib)", 1.0);
-        lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt", 1.0);
-        lines<4, 256, 16, 32, false, true, 0, 1>(c, "k4 256x16 lines32 ntload", 1.0);
-        lines<4, 256, 16, 32, false, true, 0, 3>(c, "k4 256x16 lines32 nt again", 1.0);
-        lines<4, 1024, 16, 32, false, true, 0, 3>(c, "k4 1024x16 lines32 nt", 1.0);
-        lines<4, 1024, 16, 32, false, true, 0, 3>(c, "k4 1024x16 lines32 nt again", 1.0);
+        lines<4, 256, 16, 32, false, 3>(c, "k4 256x16 lines32 nt", 1.0);
+        lines<4, 256, 16, 32, false, 1>(c, "k4 256x16 lines32 ntload", 1.0);
+        lines<4, 256, 16, 32, false, 3>(c, "k4 256x16 lines32 nt again", 1.0);
+        lines<4, 1024, 16, 32, false, 3>(c, "k4 1024x16 lines32 nt", 1.0);
+        lines<4, 1024, 16, 32, false, 3>(c, "k4 1024x16 lines32 nt again", 1.0);
         c.have_ref = false;
         variant<3, 512, 16, false, kRankAtomic, 4>(c, "k3 512x16 atomic w4 (lib)", 1.0);
-        lines<3, 256, 16, 32, false, true, 0, 3>(c, "k3 256x16 lines32 nt", 1.0);
+        lines<3, 256, 16, 32, false, 3>(c, "k3 256x16 lines32 nt", 1.0);
         c.have_ref = false;
         variant<2, 512, 16, false, kRankAtomic, 4>(c, "k2 512x16 atomic w4 (lib)", 1.0);
-        lines<2, 256, 16, 32, false, true, 0, 3>(c, "k2 256x16 lines32 nt", 1.0);
+        lines<2, 256, 16, 32, false, 3>(c, "k2 256x16 lines32 nt", 1.0);
         return 0;
     }
     if (getenv("LAB_P1")) {  // keys as pass 1 sees them: pass 0's output, then a pass on digit 1
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 0)", 1.0);
+        lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt (pass 0)", 1.0);
         CK(hipMemcpy(c.keys, c.out, c.n * 4, hipMemcpyDeviceToDevice));
         c.have_ref = false;
         printf("input: pass-0 output\n");
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 1)", 1.0, 8);
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt (pass 1) again", 1.0, 8);
+        lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt (pass 1)", 1.0, 8);
+        lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt (pass 1) again", 1.0, 8);
         return 0;
     }
     if (getenv("LAB_SHAPE")) {  // keys-only line kernel: 16384-key tiles as 1024x16 or 512x32
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
-        lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt", 1.0);
-        lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt again", 1.0);
-        lines<8, 512, 32, 32, false, true, 0, 3>(c, "k8 512x32 lines32 nt again", 1.0);
+        lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt", 1.0);
+        lines<8, 512, 32, 32, false, 3>(c, "k8 512x32 lines32 nt", 1.0);
+        lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt again", 1.0);
+        lines<8, 512, 32, 32, false, 3>(c, "k8 512x32 lines32 nt again", 1.0);
         return 0;
     }
     if (getenv("LAB_PAIRS2")) {  // key+value line kernel shape: 512 x 16 or 1024 x 8 (nt stores)
-        lines<8, 512, 16, 16, true, true, 0, 2>(c, "k8 pairs 512x16 lines16 ntstore", 1.0);
-        lines<8, 1024, 8, 16, true, true, 0, 2>(c, "k8 pairs 1024x8 lines16 ntstore", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 2>(c, "k8 pairs 512x16 lines16 ntstore again", 1.0);
-        lines<8, 1024, 8, 16, true, true, 0, 2>(c, "k8 pairs 1024x8 lines16 ntstore again", 1.0);
+        lines<8, 512, 16, 16, true, 2>(c, "k8 pairs 512x16 lines16 ntstore", 1.0);
+        lines<8, 1024, 8, 16, true, 2>(c, "k8 pairs 1024x8 lines16 ntstore", 1.0);
+        lines<8, 512, 16, 16, true, 2>(c, "k8 pairs 512x16 lines16 ntstore again", 1.0);
+        lines<8, 1024, 8, 16, true, 2>(c, "k8 pairs 1024x8 lines16 ntstore again", 1.0);
         return 0;
     }
     if (getenv("LAB_PAIRS")) {  // key+value line kernel: non-temporal loads / stores
-        lines<8, 512, 16, 16, true, true, 0, 0>(c, "k8 pairs 512x16 lines16", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 1>(c, "k8 pairs 512x16 lines16 ntload", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 3>(c, "k8 pairs 512x16 lines16 nt", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 2>(c, "k8 pairs 512x16 lines16 ntstore", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 0>(c, "k8 pairs 512x16 lines16 again", 1.0);
-        lines<8, 512, 16, 16, true, true, 0, 3>(c, "k8 pairs 512x16 lines16 nt again", 1.0);
+        lines<8, 512, 16, 16, true, 0>(c, "k8 pairs 512x16 lines16", 1.0);
+        lines<8, 512, 16, 16, true, 1>(c, "k8 pairs 512x16 lines16 ntload", 1.0);
+        lines<8, 512, 16, 16, true, 3>(c, "k8 pairs 512x16 lines16 nt", 1.0);
+        lines<8, 512, 16, 16, true, 2>(c, "k8 pairs 512x16 lines16 ntstore", 1.0);
+        lines<8, 512, 16, 16, true, 0>(c, "k8 pairs 512x16 lines16 again", 1.0);
+        lines<8, 512, 16, 16, true, 3>(c, "k8 pairs 512x16 lines16 nt again", 1.0);
         return 0;
     }
-    lines<8, 1024, 16, 32, false, true, 0, 3>(c, "k8 1024x16 lines32 nt", 1.0);
+    lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt", 1.0);
     return 0;
 #endif
     hist_variant<256>(c, "hist 256 x8", 256, 8);
-    hist_variant<256>(c, "hist 256 x16", 256, 16);
-    hist_variant<256>(c, "hist 256 x32", 256, 32);
     hist_variant<512>(c, "hist 512 x8", 256, 8);
-    hist_variant<512>(c, "hist 512 x16", 256, 16);
     hist_variant<1024>(c, "hist 1024 x4", 256, 4);
     hist_variant<1024>(c, "hist 1024 x8", 256, 8);
-    constexpr int M = kRankMatch;
-    constexpr int RW = kRankMatchRW;
     constexpr int CT = kRankCount;
     constexpr int AT = kRankAtomic;
-    variant<8, 256, 16, false, M, 0>(c, "k8 256x16 match (ref)", 1.0);
-    variant<8, 256, 16, false, CT, 0>(c, "k8 256x16 count", 1.0);
-    variant<8, 256, 32, false, CT, 0>(c, "k8 256x32 count", 1.0);
-    variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count", 1.0);
-    variant<8, 512, 32, false, CT, 0>(c, "k8 512x32 count x2", 2.0);
-    variant<8, 512, 32, false, CT, 0, false, 2>(c, "k8 512x32 count nostore", 1.0);
-    variant<8, 512, 32, false, AT, 0>(c, "k8 512x32 atomic", 1.0);
-    variant<8, 512, 32, false, AT, 0>(c, "k8 512x32 atomic x2", 2.0);
-    variant<8, 512, 32, false, AT, 0, false, 2>(c, "k8 512x32 atomic nostore", 1.0);
-    variant<8, 256, 32, false, AT, 0>(c, "k8 256x32 atomic", 1.0);
-    variant<8, 512, 16, false, AT, 0>(c, "k8 512x16 atomic", 1.0);
-    variant<8, 256, 16, false, AT, 0>(c, "k8 256x16 atomic", 1.0);
-    variant<8, 512, 16, false, AT, 0, false, 0, 32>(c, "k8 512x16 atomic wc32", 1.0);
-    variant<8, 512, 16, false, AT, 0, false, 0, 16>(c, "k8 512x16 atomic wc16", 1.0);
-    variant<8, 512, 24, false, AT, 0, false, 0, 16>(c, "k8 512x24 atomic wc16", 1.0);
-    variant<8, 512, 32, false, AT, 0, false, 0, 16>(c, "k8 512x32 atomic wc16", 1.0);
-    variant<8, 512, 32, false, AT, 0, false, 0, 32>(c, "k8 512x32 atomic wc32", 1.0);
-    variant<8, 1024, 16, false, AT, 0, false, 0, 32>(c, "k8 1024x16 atomic wc32", 1.0);
-    variant<8, 1024, 24, false, AT, 0, false, 0, 32>(c, "k8 1024x24 atomic wc32", 1.0);
-    variant<8, 256, 32, false, AT, 0, false, 0, 32>(c, "k8 256x32 atomic wc32", 1.0);
-    variant<8, 512, 16, false, AT, 0, false, 2, 32>(c, "k8 512x16 atomic wc32 nostore", 1.0);
-    lines<8, 1024, 16, 32, false, false>(c, "k8 1024x16 lines32", 1.0);
-    lines<8, 1024, 16, 16, false>(c, "k8 1024x16 lines16", 1.0);
-    lines<8, 1024, 16, 16, false, false>(c, "k8 1024x16 lines16 cf", 1.0);
-    lines<8, 1024, 16, 16, false, true, 2>(c, "k8 1024x16 lines16 nostore", 1.0);
-    lines<8, 1024, 16, 16, false, true, 4>(c, "k8 1024x16 lines16 plainadd", 1.0);
-    lines<8, 1024, 16, 16, false, true, 6>(c, "k8 1024x16 lines16 plainadd nostore", 1.0);
-    lines<8, 512, 32, 16, false>(c, "k8 512x32 lines16", 1.0);
-    lines<8, 512, 32, 16, false, true, 2>(c, "k8 512x32 lines16 nostore", 1.0);
-    lines<8, 512, 16, 16, false, false>(c, "k8 512x16 lines16 cf", 1.0);
-    lines<8, 512, 16, 32, false>(c, "k8 512x16 lines32", 1.0);
-    lines<8, 512, 16, 16, false>(c, "k8 512x16 lines16", 1.0);
-    lines<8, 512, 24, 16, false>(c, "k8 512x24 lines16", 1.0);
-    lines<8, 1024, 8, 32, false>(c, "k8 1024x8 lines32", 1.0);
-    lines<8, 256, 32, 32, false>(c, "k8 256x32 lines32", 1.0);
-    variant<8, 256, 64, false, CT, 0>(c, "k8 256x64 count", 1.0);
-    variant<8, 1024, 16, false, CT, 0>(c, "k8 1024x16 count", 1.0);
+    variant<8, 512, 16, false, AT, 0>(c, "k8 512x16 atomic (rs_scatter)", 1.0);
+    variant<8, 512, 16, false, CT, 0>(c, "k8 512x16 ballot (rs_scatter)", 1.0);
+    lines<8, 1024, 16, 32, false, 3>(c, "k8 1024x16 lines32 nt (lib)", 1.0);
     c.have_ref = false;
-    variant<8, 256, 16, true, M, 0>(c, "k8 pairs 256x16 match (ref)", 1.0);
-    variant<8, 512, 16, true, RW, 0>(c, "k8 pairs 512x16 matchRW", 1.0);
-    variant<8, 256, 32, true, RW, 0>(c, "k8 pairs 256x32 matchRW", 1.0);
-    variant<8, 512, 16, true, CT, 0>(c, "k8 pairs 512x16 count", 1.0);
-    variant<8, 512, 32, true, CT, 0>(c, "k8 pairs 512x32 count", 1.0);
-    variant<8, 512, 32, true, AT, 0>(c, "k8 pairs 512x32 atomic", 1.0);
-    variant<8, 512, 16, true, AT, 0>(c, "k8 pairs 512x16 atomic", 1.0);
-    variant<8, 512, 16, true, AT, 0, false, 0, 32>(c, "k8 pairs 512x16 atomic wc32", 1.0);
-    lines<8, 1024, 8, 16, true, false>(c, "k8 pairs 1024x8 lines16", 1.0);
-    lines<8, 512, 16, 16, true>(c, "k8 pairs 512x16 lines16", 1.0);
+    variant<8, 512, 16, true, AT, 0>(c, "k8 pairs 512x16 atomic (rs_scatter)", 1.0);
+    lines<8, 512, 16, 16, true, 2>(c, "k8 pairs 512x16 lines16 ntstore (lib)", 1.0);
     c.have_ref = false;
-    variant<4, 256, 16, false, M, 0>(c, "k4 256x16 match (ref)", 1.0);
-    variant<4, 256, 16, false, CT, 0>(c, "k4 256x16 count", 1.0);
-    variant<4, 512, 16, false, CT, 4>(c, "k4 512x16 count w4", 1.0);
-    variant<4, 512, 32, false, CT, 0>(c, "k4 512x32 count", 1.0);
-    variant<4, 512, 16, false, AT, 0>(c, "k4 512x16 atomic", 1.0);
-    variant<4, 512, 32, false, AT, 0>(c, "k4 512x32 atomic", 1.0);
-    variant<4, 512, 16, false, AT, 0, false, 0, 32>(c, "k4 512x16 atomic wc32", 1.0);
-    variant<4, 512, 32, false, AT, 0, false, 0, 32>(c, "k4 512x32 atomic wc32", 1.0);
-    lines<4, 1024, 16, 32, false>(c, "k4 1024x16 lines32", 1.0);
-    lines<4, 1024, 32, 32, false>(c, "k4 1024x32 lines32", 1.0);
-    lines<4, 512, 32, 32, false>(c, "k4 512x32 lines32", 1.0);
-    lines<4, 512, 16, 32, false>(c, "k4 512x16 lines32", 1.0);
+    variant<4, 512, 16, false, AT, 4>(c, "k4 512x16 atomic w4", 1.0);
+    lines<4, 256, 16, 32, false, 3>(c, "k4 256x16 lines32 nt (lib)", 1.0);
+    lines<4, 1024, 16, 32, false, 3>(c, "k4 1024x16 lines32 nt (lib, n >= 2^28)", 1.0);
     return 0;
 }

@@ -53,10 +53,14 @@ inline void sortByDevice(const uint32_t *h_input, int n, uint32_t *h_output, int
     rsort_phase_times t;
     RSORT_CHECK(rsort_u32_ex(h_input, h_output, (int64_t)n, numBits, blockSize, &t));
 #ifdef RSORT_MEASURE_PORTION_EXECUTION_TIME
-    printf(">>>> Time | Sort locally blocks   : %.3f\n", 0.0);
+    // The reference's four phase lines (Parallel7.cu:633-638), measured by hipEvents around every
+    // launch of this call. The block-local sort is not a separate kernel here: it is fused into
+    // the scatter pass (each tile is ranked and staged in LDS, then written), so its time is
+    // inside "Scatter" and its own line reads 0 with a note (numeric parsers see %.3f first).
+    printf(">>>> Time | Sort locally blocks   : %.3f (fused into Scatter)\n", 0.0);
     printf(">>>> Time | Histogram             : %.3f\n", t.ms[RSORT_PHASE_HISTOGRAM]);
     printf(">>>> Time | Scan                  : %.3f\n", t.ms[RSORT_PHASE_SCAN]);
-    printf(">>>> Time | Scatter               : %.3f\n", t.ms[RSORT_PHASE_SCATTER]);
+    printf(">>>> Time | Scatter               : %.3f\n", t.ms[RSORT_PHASE_SCATTER] + t.ms[RSORT_PHASE_COPY]);
 #endif
 }
 

@@ -22,7 +22,7 @@
  *                        key-range partition step (BASELINE config 5)
  *
  * Semantics shared by every sort entry point:
- *   - keys are uint32_t, sorted ascending; k_bits in [1, 12] digit bits per pass, passes at
+ *   - keys are uint32_t, sorted ascending; k_bits in [1, 13] digit bits per pass (13: the reference's SMEM limit), passes at
  *     bit 0, k, 2k, ... < 32 (the last digit is short when k does not divide 32, exactly as
  *     Baseline1.cu:30-49);
  *   - output is bit-exact with Baseline1.cu's sortByHost; pairs are STABLE (equal keys keep
@@ -52,7 +52,7 @@ extern "C" {
 typedef enum rsort_status {
     RSORT_OK = 0,
     RSORT_ERR_ARG = 1,        /* NULL pointer where data is required, bad option value */
-    RSORT_ERR_BITS = 2,       /* k_bits outside [1, 12] */
+    RSORT_ERR_BITS = 2,       /* k_bits outside [1, 13] */
     RSORT_ERR_SIZE = 3,       /* n < 0 or n >= 2^32 */
     RSORT_ERR_ALIGN = 4,      /* device buffer not 4-byte aligned */
     RSORT_ERR_ALLOC = 5,      /* hipMalloc / host allocation failed */

@@ -37,7 +37,7 @@ def test_status_strings():
     lib = rs._lib()
     for st in range(9):
         assert lib.rsort_status_string(st)
-    assert lib.rsort_status_string(2) == b"k_bits outside [1, 12]"
+    assert lib.rsort_status_string(2) == b"k_bits outside [1, 13]"
 
 
 @pytest.mark.parametrize("n,k", [(0, 8), (1, 8), (513, 4), ((1 << 24) + 1, 8), (1 << 26, 4), (1 << 30, 8),
@@ -67,7 +67,7 @@ def test_plan_explicit_tiles_per_chunk():
     assert p.num_chunks == -(-256 // 7)
 
 
-@pytest.mark.parametrize("n,k,status", [(10, 0, 2), (10, 13, 2), (-1, 8, 3), (1 << 32, 8, 3)])
+@pytest.mark.parametrize("n,k,status", [(10, 0, 2), (10, 14, 2), (-1, 8, 3), (1 << 32, 8, 3)])
 def test_plan_rejects(n, k, status):
     with pytest.raises(rs.RSortError) as e:
         rs.plan(n, k)
@@ -100,7 +100,7 @@ def test_python_mirror_error_behaviour():
     with pytest.raises(TypeError):
         rs.sortByDevice(np.zeros(4, np.int64), 4, np.zeros(4, np.uint32), 8)
     with pytest.raises(rs.RSortError) as e:
-        rs.sortByDevice(np.zeros(4, np.uint32), 4, np.zeros(4, np.uint32), 13)
+        rs.sortByDevice(np.zeros(4, np.uint32), 4, np.zeros(4, np.uint32), 14)
     assert e.value.status == 2
 
 

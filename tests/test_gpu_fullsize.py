@@ -65,3 +65,25 @@ def test_fullsize_pairs_zipf():
     same = ko[1:] == ko[:-1]
     assert bool((idx[1:][same] > idx[:-1][same]).all())     # stable
     assert fingerprint(ko) == fingerprint(keys)
+
+
+@pytest.mark.parametrize("dist_name", ["uniform", "zipf"])
+def test_fullsize_ballot_ranking_agrees(dist_name):
+    """C3 size through RSORT_RANK_BALLOT (wave64 ballot peer match, no lane-order premise) and
+    through the default lane-ordered LDS-add ranking: two independent rankings, one unique sorted
+    output -- bit-identical, sorted, same multiset (VERDICT r1 #7)."""
+    n = 1 << 30
+    keys = rs.empty_u32(n)
+    if dist_name == "uniform":
+        rs.gen_uniform(keys, 0xB411)
+    else:
+        rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32()), 0xB411)
+    out = rs.empty_u32(n)
+    rs.sort_device(keys, out, 8)
+    fp_default = rs.fingerprint(out)
+    with rs.rank_algo(rs.RANK_BALLOT):
+        out_b = rs.empty_u32(n)
+        rs.sort_device(keys, out_b, 8)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_b)
+    assert fp_default == (rs.fingerprint(keys)[0], 0)
