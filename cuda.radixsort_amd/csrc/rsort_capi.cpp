@@ -120,6 +120,14 @@ bool joint_plan(const rsort_plan &p) {
            (geom_from_shape(p.threads, p.tile_keys, p.pairs) == (p.pairs ? kGeomLinesPairs : kGeomLines));
 }
 
+// Next-digit counts (rs_scatter_lines, k = 3, 4 keys): each pass adds the next pass's chunk table
+// from where it writes every key, so only pass 0 reads keys for a histogram. Needs the line
+// kernel (lane-ordered ranks, 16-B aligned outputs: checked per sort) and a second table.
+bool next_plan(const rsort_plan &p) {
+    const int g = geom_from_shape(p.threads, p.tile_keys, p.pairs);
+    return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 && (g == kGeomSmall || g == kGeomLines);
+}
+
 int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int partition = 0) {
     if (!p) return RSORT_ERR_ARG;
     if (k < kMinBits || k > kMaxBits) return RSORT_ERR_BITS;
@@ -161,6 +169,7 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
         ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
         ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
     }
+    if (!partition && next_plan(*p)) ws += align256((size_t)p->table_entries * 4);  // the next pass's table
     p->workspace_bytes = ws;
     return RSORT_OK;
 }
@@ -176,7 +185,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *table2;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -198,7 +207,9 @@ Carve carve(const rsort_plan &p, void *ws) {
         c.joint = (uint32_t *)q;
         q += align256((size_t)kJointBins * kJointBins * 4);
         c.bounds = (uint32_t *)q;
+        q += align256((size_t)2 * kBoundsWords * 4);
     }
+    if (next_plan(p)) c.table2 = (uint32_t *)q;
     return c;
 }
 
@@ -254,10 +265,12 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     return hip_status(launch_histogram(p.k_bits, dmode, a, s));
 }
 
-int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s) {
+int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr) {
     ScanArgs a{};
     a.table = table;
     a.block_sums = bsums;
+    a.zero = zero;
+    a.zero_n = zero ? (uint64_t)p.table_entries : 0u;
     a.m = (uint64_t)p.table_entries;
     a.nblocks = (uint32_t)p.scan_blocks;
     PhaseScope ps(RSORT_PHASE_SCAN, p.table_entries, s);
@@ -266,9 +279,11 @@ int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s
 
 int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
-               const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr) {
+               const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr,
+               uint32_t *next_table = nullptr) {
     ScatterArgs a{};
     a.bounds = bounds;
+    a.next_table = next_table;
     a.kin = kin;
     a.vin = vin;
     a.kout = kout;
@@ -285,8 +300,8 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
-    if (bounds && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
-        return RSORT_ERR_ARG;  // group chunks: rs_scatter_lines only
+    if ((bounds || next_table) && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
+        return RSORT_ERR_ARG;  // group chunks, next-digit counts: rs_scatter_lines only
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
     return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, local_only ? 0 : aligned16, a, s));
 }
@@ -337,6 +352,9 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     if (joint_plan(p) && !joint &&
         hipMemsetAsync(c.bounds, 0, (size_t)2 * kBoundsWords * 4, s) != hipSuccess)  // rsort_group_flags: none
         return RSORT_ERR_HIP;
+    // next-digit counts (k = 3, 4): the same kernel conditions as digit groups
+    const bool nextc = next_plan(p) && g_group_chunks.load() != 0 && internal_rank(g_rank_algo.load()) == kRankAtomic &&
+                       ((((uintptr_t)kout) | (uintptr_t)c.tmp_k) & 15u) == 0;
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
         const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
@@ -345,16 +363,20 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // even pass i counts the joint counts for pass i + 1; odd pass i may use them
         const bool count_joint = joint && (i % 2 == 0) && i + 1 < P;
         const uint32_t *bounds = (joint && (i % 2 == 1)) ? c.bounds + (i / 2) * kBoundsWords : nullptr;
+        // next-digit plans alternate two tables: pass i reads tab, adds pass i + 1's into nxt
+        uint32_t *tab = (nextc && (i % 2 == 1)) ? c.table2 : c.table;
+        uint32_t *nxt = (nextc && i + 1 < P) ? ((i % 2 == 1) ? c.table : c.table2) : nullptr;
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
                                          c.bounds + (i / 2) * kBoundsWords, s)))
                 return st;
-        } else if ((st = do_histogram(p, sk, shift, c.table, kDigitShift, nullptr, 0, s, bounds, c.joint))) {
+        } else if (!(nextc && i > 0) &&
+                   (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint))) {
             return st;
         }
-        if ((st = do_scan(p, c.table, c.bsums, s))) return st;
-        if ((st = do_scatter(p, sk, sv, dk, dv, shift, c.table, 0, kDigitShift, nullptr, 0, s, bounds)))
+        if ((st = do_scan(p, tab, c.bsums, s, nxt))) return st;
+        if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt)))
             return st;
         sk = dk;
         sv = dv;

@@ -98,6 +98,9 @@ struct ScatterArgs {
     // [bounds[1 + c], bounds[2 + c]) (a digit group of the previous pass) instead of
     // [c * chunk_keys, (c + 1) * chunk_keys)
     const uint32_t *bounds;
+    // rs_scatter_lines with k <= 4 only: != nullptr -> the next pass's chunk table (zeroed), into
+    // which this pass adds every written key's next digit by its destination chunk
+    uint32_t *next_table;
 };
 
 struct ScanArgs {
@@ -105,6 +108,8 @@ struct ScanArgs {
     uint32_t *block_sums;
     uint64_t m;             // table entries
     uint32_t nblocks;
+    uint32_t *zero;         // optional: zero_n words cleared by the first launch
+    uint64_t zero_n;
 };
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.

@@ -404,6 +404,10 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
 // L2) and scans itself.
 __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
     __shared__ uint32_t s_ws[kScanThreads / kWave];
+    // next-digit plans: clear the table the coming scatter counts into (read by the previous
+    // pass's scatter, finished before this launch)
+    for (uint64_t i = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x; i < a.zero_n; i += (uint64_t)gridDim.x * kScanThreads)
+        a.zero[i] = 0u;
     const uint64_t base = (uint64_t)blockIdx.x * kScanSegment + (uint64_t)threadIdx.x * kScanPerThread;
     uint32_t s = 0;
 #pragma unroll
@@ -793,6 +797,20 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
+    // Next-digit counts (k <= 4 with a.next_table): the NEXT pass's chunk table, counted here by
+    // where each key is written. Digit d's keys of this chunk land in [table[d][c], + count) --
+    // at most chunk_keys keys, so in at most two of the next pass's chunks (same plan, same
+    // chunks): s_next[(d * 2 + slot) * R + next digit], slot 1 from position s_nb[d] on. The
+    // next pass then reads no keys for its histogram.
+    // NXR replicas of every counter, picked by lane % NXR: the lanes of one output instruction mostly
+    // share (digit, slot) -- a digit's lines are adjacent -- so without them ~4 lanes would hit
+    // each of the R counters and serialise in the LDS
+    constexpr bool NX = (R <= 16) && DMODE == kDigitShift;
+    constexpr uint32_t NXR = 8;
+    __shared__ uint32_t s_next[NX ? 2 * R * R * NXR : 1];
+    __shared__ uint32_t s_nb[NX ? R : 1];  // first position of digit d's second output chunk
+    __shared__ uint32_t s_oc[NX ? R : 1];  // digit d's first output chunk
+    const bool count_next = NX && a.next_table != nullptr;
 
     const uint32_t t = threadIdx.x;
     const uint32_t w = t / kWave;
@@ -830,7 +848,23 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         if constexpr (DMODE == kDigitSplit)
             ik = (d_own == 0 || a.nsplit == 0) ? 0u : a.splitters[min(d_own, a.nsplit) - 1u];
         for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = ik;
+        if constexpr (NX) {
+            if (count_next) {
+                const uint64_t oc = (uint64_t)g / a.chunk_keys;
+                s_oc[d_own] = (uint32_t)oc;
+                s_nb[d_own] = (uint32_t)min<uint64_t>((oc + 1) * a.chunk_keys, 0xFFFFFFFFull);
+            }
+        }
     }
+    if constexpr (NX) {
+        if (count_next)
+            for (uint32_t i = t; i < 2 * R * R * NXR; i += THREADS) s_next[i] = 0;
+    }
+    // one written key of digit d at global position gp: count its next digit (k <= 4 plans)
+    auto next_add = [&](uint32_t d, uint32_t slot, uint32_t key) {
+        const uint32_t e = (key >> (a.shift + BITS)) & (R - 1u);
+        atomicAdd(&s_next[((d * 2 + slot) * R + e) * NXR + (lane & (NXR - 1))], 1u);
+    };
 
     const uint32_t base = w * SEG + lane;
     auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
@@ -859,9 +893,18 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 
     // one 16-B quad of line L at quad offset q -> global; every key of an LDS line has the line's
     // digit, which locates the line's segment record (info)
-    auto store_quad = [&](uint32_t L, uint32_t q, const u32x4 &kv, const u32x4 &vv, const uint2 &info) {
+    auto store_quad = [&](uint32_t L, uint32_t q, const u32x4 &kv, const u32x4 &vv, const uint2 &info, uint32_t d) {
         const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
         const uint64_t gp = (uint64_t)(info.x + L * G + q);
+        if constexpr (NX) {
+            if (count_next) {
+                // a quad never straddles a chunk boundary (both are multiples of 4 keys)
+                const uint32_t slot = (uint32_t)gp >= s_nb[d] ? 1u : 0u;
+#pragma unroll
+                for (uint32_t x = 0; x < 4; ++x)
+                    if (lo <= q + x) next_add(d, slot, kv[x]);
+            }
+        }
         if (lo <= q) {
             if constexpr ((NT & 2) != 0) {  // non-temporal whole-line stores
                 __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
@@ -895,10 +938,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             vv0 = *reinterpret_cast<const u32x4 *>(&s_vstage[L0 * G + q0]);
             if (two) vv1 = *reinterpret_cast<const u32x4 *>(&s_vstage[L1 * G + q1]);
         }
-        const uint2 in0 = s_out[dig(kv0.x)];
-        const uint2 in1 = s_out[dig(kv1.x)];
-        store_quad(L0, q0, kv0, vv0, in0);
-        if (two) store_quad(L1, q1, kv1, vv1, in1);
+        const uint32_t d0 = dig(kv0.x), d1 = dig(kv1.x);
+        const uint2 in0 = s_out[d0];
+        const uint2 in1 = s_out[d1];
+        store_quad(L0, q0, kv0, vv0, in0, d0);
+        if (two) store_quad(L1, q1, kv1, vv1, in1, d1);
     };
 
     uint32_t key[KPT];
@@ -1098,8 +1142,27 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             const uint2 fl = s_flush[item / G];
             const uint32_t x = item % G;
             if ((fl.y & 0xFFu) <= x && x < (fl.y >> 8)) {
-                a.kout[(uint64_t)fl.x + x] = s_stage[CAP + item];
+                const uint32_t k = s_stage[CAP + item];
+                a.kout[(uint64_t)fl.x + x] = k;
                 if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_vstage[CAP + item];
+                if constexpr (NX) {
+                    const uint32_t d = item / G;
+                    if (count_next) next_add(d, fl.x + x >= s_nb[d] ? 1u : 0u, k);
+                }
+            }
+        }
+    }
+    if constexpr (NX) {
+        if (count_next) {
+            __syncthreads();
+            for (uint32_t i = t; i < 2 * R * R; i += THREADS) {
+                uint32_t v = 0;
+#pragma unroll
+                for (uint32_t r = 0; r < NXR; ++r) v += s_next[i * NXR + r];
+                if (v) {
+                    const uint32_t d = i / (2 * R), slot = (i / R) % 2, e = i % R;
+                    atomicAdd(&a.next_table[(uint64_t)e * a.num_chunks + s_oc[d] + slot], v);
+                }
             }
         }
     }

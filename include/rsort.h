@@ -166,10 +166,13 @@ RSORT_API int rsort_pass_local_sort(const rsort_plan *plan, const uint32_t *d_ke
 /* ---------------------------------------------------------------- options / profiling */
 RSORT_API int rsort_set_rank_algo(int algo); /* rsort_rank_algo, process-wide */
 RSORT_API int rsort_get_rank_algo(void);
-/* Digit-group chunks (default on): for k = 8 plans with 256 chunks, every second pass takes
- * the previous pass's digit groups as its chunks and reads no keys for its histogram (the
- * pass before counts (digit, next digit) pairs while it reads them). Off: every pass counts
- * its own histogram. Same output either way; process-wide. */
+/* Histograms carried between passes (default on), so passes read no keys for their histogram:
+ *  - k = 8 plans with 256 chunks (digit-group chunks): every second pass takes the previous
+ *    pass's digit groups as its chunks (the pass before counts (digit, next digit) pairs while
+ *    it reads the keys);
+ *  - k = 3, 4 keys-only plans (next-digit counts): every pass adds the next pass's chunk table
+ *    from where it writes each key; only pass 0 reads keys for a histogram.
+ * Off: every pass counts its own histogram. Same output either way; process-wide. */
 RSORT_API int rsort_set_group_chunks(int enable);
 RSORT_API int rsort_get_group_chunks(void);
 /* After a sort with `plan` and `d_workspace` has completed on `stream`: flags[i] = 1 if odd pass

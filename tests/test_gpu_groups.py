@@ -154,3 +154,48 @@ def test_unaligned_output_falls_back():
     rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
     assert rs.group_flags(p, ws) == [0, 0]
     assert np.array_equal(rs.to_numpy_u32(d_out), oracle_sort(x, 8))
+
+
+# ------------------------------------------------------------------ next-digit counts (k = 3, 4)
+def _keys(dist, n, seed):
+    if dist == "uniform":
+        return uniform_keys(n, seed=seed)
+    if dist == "zipf":
+        return zipf_keys(n, seed=seed)
+    if dist == "allsame":
+        return np.full(n, 0x9E3779B9, np.uint32)
+    if dist == "sorted":
+        return np.sort(uniform_keys(n, seed=seed))
+    if dist == "reversed":
+        return np.sort(uniform_keys(n, seed=seed))[::-1].copy()
+    return uniform_keys(n, seed=seed) & np.uint32(0x0F0F00FF)  # "sparse": many empty digits
+
+
+@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("dist", ["uniform", "zipf", "allsame", "sorted", "reversed", "sparse"])
+@pytest.mark.parametrize("n", [4096 * 40 + 3, (1 << 21) + 517])
+def test_next_digit_counts(k, dist, n):
+    """k = 3, 4 keys-only plans: every pass adds the next pass's chunk table from where it writes
+    each key (rs_scatter_lines, a.next_table), so passes 1.. read no keys for their histogram --
+    bit-exact against the oracle with the path on and off, on balanced and extreme inputs (one
+    digit holding a whole chunk spans two of the next pass's chunks)."""
+    x = _keys(dist, n, n + k)
+    want = oracle_sort(x, k)
+    for on in (True, False):
+        with rs.group_chunks(on):
+            d_in = rs.from_numpy_u32(x)
+            d_out = rs.empty_u32(n)
+            rs.sort_device(d_in, d_out, k)
+            assert np.array_equal(rs.to_numpy_u32(d_out), want), (k, dist, n, on)
+
+
+@pytest.mark.parametrize("tpc", [1, 3, 17])
+def test_next_digit_counts_chunk_geometries(tpc):
+    """Small chunks (one tile per chunk and up): digit ranges cross the next pass's chunk
+    boundaries in every tile."""
+    n = 4096 * 97 + 11
+    x = zipf_keys(n, seed=tpc)
+    p = rs.plan(n, 4, False, tpc)
+    d_out = rs.empty_u32(n)
+    rs.sort_device(rs.from_numpy_u32(x), d_out, 4, plan_=p)
+    assert np.array_equal(rs.to_numpy_u32(d_out), oracle_sort(x, 4))

@@ -272,7 +272,8 @@ def test_host_entry_and_reference_dispatcher(golden, capsys):
     times = {}
     rs.sortByDevice(x, x.size, y, 4, 512, times=times)
     assert y.tolist() == case["output"]
-    assert times["scatter"]["launches"] == 8 and times["histogram"]["launches"] == 8
+    # k = 4: 8 scatter passes; one key-reading histogram (the next-digit counts carry the rest)
+    assert times["scatter"]["launches"] == 8 and times["histogram"]["launches"] == 1
     z = np.zeros_like(x)
     rs.sort(x, x.size, z, rs.SORT_BY_DEVICE, 4, 512)
     out = capsys.readouterr().out
