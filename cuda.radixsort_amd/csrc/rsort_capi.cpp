@@ -169,7 +169,10 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
         ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
         ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
     }
-    if (!partition && next_plan(*p)) ws += align256((size_t)p->table_entries * 4);  // the next pass's table
+    if (!partition && next_plan(*p)) {
+        ws += align256((size_t)p->table_entries * 4);  // the next pass's table
+        ws += 256;                                     // the tail-scan counter
+    }
     p->workspace_bytes = ws;
     return RSORT_OK;
 }
@@ -185,7 +188,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *table2;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *table2, *done;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -209,7 +212,11 @@ Carve carve(const rsort_plan &p, void *ws) {
         c.bounds = (uint32_t *)q;
         q += align256((size_t)2 * kBoundsWords * 4);
     }
-    if (next_plan(p)) c.table2 = (uint32_t *)q;
+    if (next_plan(p)) {
+        c.table2 = (uint32_t *)q;
+        q += align256((size_t)p.table_entries * 4);
+        c.done = (uint32_t *)q;
+    }
     return c;
 }
 
@@ -265,8 +272,10 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     return hip_status(launch_histogram(p.k_bits, dmode, a, s));
 }
 
-int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr) {
+int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr,
+            uint32_t *done = nullptr) {
     ScanArgs a{};
+    a.done = done;
     a.table = table;
     a.block_sums = bsums;
     a.zero = zero;
@@ -280,10 +289,12 @@ int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s
 int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
                const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr,
-               uint32_t *next_table = nullptr) {
+               uint32_t *next_table = nullptr, uint32_t *tail_zero = nullptr, uint32_t *done = nullptr) {
     ScatterArgs a{};
     a.bounds = bounds;
     a.next_table = next_table;
+    a.tail_zero = tail_zero;
+    a.done = done;
     a.kin = kin;
     a.vin = vin;
     a.kout = kout;
@@ -375,8 +386,11 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint))) {
             return st;
         }
-        if ((st = do_scan(p, tab, c.bsums, s, nxt))) return st;
-        if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt)))
+        // next-digit plans: pass 0's table is scanned by launches (which also arm the tail
+        // counter); every later table was scanned by the previous scatter's last workgroup
+        if (!(nextc && i > 0) && (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr))) return st;
+        if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt,
+                             nxt ? tab : nullptr, nxt ? c.done : nullptr)))
             return st;
         sk = dk;
         sv = dv;

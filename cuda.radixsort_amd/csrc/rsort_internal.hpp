@@ -101,6 +101,11 @@ struct ScatterArgs {
     // rs_scatter_lines with k <= 4 only: != nullptr -> the next pass's chunk table (zeroed), into
     // which this pass adds every written key's next digit by its destination chunk
     uint32_t *next_table;
+    // with next_table: the workgroup that finishes last scans next_table in place (exclusive,
+    // the rs_scan_* result), clears tail_zero (the table the next pass counts into; this pass's
+    // own, read by every workgroup before it finished) and re-arms *done (zero on entry)
+    uint32_t *tail_zero;
+    uint32_t *done;
 };
 
 struct ScanArgs {
@@ -110,6 +115,7 @@ struct ScanArgs {
     uint32_t nblocks;
     uint32_t *zero;         // optional: zero_n words cleared by the first launch
     uint64_t zero_n;
+    uint32_t *done;         // optional: a tail-scan counter (ScatterArgs::done) zeroed by the first launch
 };
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.

@@ -408,6 +408,7 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
     // pass's scatter, finished before this launch)
     for (uint64_t i = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x; i < a.zero_n; i += (uint64_t)gridDim.x * kScanThreads)
         a.zero[i] = 0u;
+    if (a.done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.done = 0u;
     const uint64_t base = (uint64_t)blockIdx.x * kScanSegment + (uint64_t)threadIdx.x * kScanPerThread;
     uint32_t s = 0;
 #pragma unroll
@@ -440,6 +441,67 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
         if (base + i < a.m) a.table[base + i] = run;
         run += v[i];
     }
+}
+
+// The same exclusive scan as the tail of a kernel whose workgroups ADD into `table` with agent-scope
+// atomics (m entries, a multiple of 4, 16-B aligned): every workgroup waits for its adds and bumps
+// *done; the one whose bump comes last scans the table alone -- each thread a contiguous run of
+// m / THREADS entries -- clears `zero` (m entries) and re-arms *done. Next-digit plans (k = 3, 4)
+// scan every table after the first this way: one launch per pass instead of three (rs_scan_reduce
+// + rs_scan_down, each ~5 us at C2, and their launch gaps).
+// Visibility (MI355X_MICROARCH.md, inter-workgroup visibility): atomics are performed beyond the
+// XCD's L2 and drop the line from it, nothing reads the table before the last workgroup does, and
+// that workgroup reads it with sc1 loads behind an agent acquire. The producers need no release
+// fence: a `buffer_wbl2` per workgroup (what __threadfence() issues) wrote back the default-policy
+// output held in L2 once per workgroup and doubled the C2 pass time. All threads must call it.
+template <int THREADS>
+__device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t *done, uint32_t *s_ws,
+                          uint32_t *s_flag) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t t = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds have been performed
+    __syncthreads();
+    if (t == 0) *s_flag = atomicAdd(done, 1u) == gridDim.x - 1u ? 1u : 0u;
+    __syncthreads();
+    if (*s_flag == 0u) return;
+    // the acquire invalidates this CU's L1; no L2 holds a copy of the table (atomics drop the line,
+    // and nothing loaded it in this launch), so plain 16-B loads see every add
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint64_t per = ((m + THREADS - 1) / THREADS + 3) & ~(uint64_t)3;
+    const uint32_t beg = (uint32_t)(min(m, (uint64_t)t * per) / 4), end = (uint32_t)(min(m, (uint64_t)t * per + per) / 4);
+    u32x4 *q = reinterpret_cast<u32x4 *>(table);
+    // batches of 8 quads in flight (a latency-bound sweep: m = 20480 at C2 is 20 quads per thread)
+    constexpr uint32_t B = 8;
+    uint32_t s = 0;
+    for (uint32_t i0 = beg; i0 < end; i0 += B) {
+        u32x4 v[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? q[i0 + u] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<THREADS>(s, s_ws, tot);
+    for (uint32_t i0 = beg; i0 < end; i0 += B) {
+        u32x4 v[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? q[i0 + u] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t u = 0; u < B; ++u) {
+            u32x4 o;
+            o.x = run;
+            o.y = run + v[u].x;
+            o.z = o.y + v[u].y;
+            o.w = o.z + v[u].z;
+            run = o.w + v[u].w;
+            if (i0 + u < end) q[i0 + u] = o;
+        }
+    }
+    u32x4 *z = reinterpret_cast<u32x4 *>(zero);
+    for (uint64_t i = t; i < m / 4; i += THREADS) z[i] = u32x4{0u, 0u, 0u, 0u};
+    if (t == 0) *done = 0u;
 }
 
 // ------------------------------------------------------------------------------ group bounds
@@ -1163,6 +1225,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                     const uint32_t d = i / (2 * R), slot = (i / R) % 2, e = i % R;
                     atomicAdd(&a.next_table[(uint64_t)e * a.num_chunks + s_oc[d] + slot], v);
                 }
+            }
+            // the last workgroup scans the next pass's table (no scan launches between passes)
+            if (a.done != nullptr) {
+                __shared__ uint32_t s_last;
+                tail_scan<THREADS>(a.next_table, (uint64_t)R * a.num_chunks, a.tail_zero, a.done, s_ws, &s_last);
             }
         }
     }
