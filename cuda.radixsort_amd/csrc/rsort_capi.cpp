@@ -289,8 +289,10 @@ int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s
 int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
                const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr,
-               uint32_t *next_table = nullptr, uint32_t *tail_zero = nullptr, uint32_t *done = nullptr) {
+               uint32_t *next_table = nullptr, uint32_t *tail_zero = nullptr, uint32_t *done = nullptr,
+               const uint32_t *cl_select = nullptr) {
     ScatterArgs a{};
+    a.cl_select = cl_select;
     a.bounds = bounds;
     a.next_table = next_table;
     a.tail_zero = tail_zero;
@@ -389,8 +391,12 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // next-digit plans: pass 0's table is scanned by launches (which also arm the tail
         // counter); every later table was scanned by the previous scatter's last workgroup
         if (!(nextc && i > 0) && (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr))) return st;
+        // passes after the first of a digit-group sort: where the previous odd pass's groups were
+        // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the
+        // clustered-input kernel runs (rank_add_hot), else the plain one -- chosen on the device
+        const uint32_t *cl = (joint && i >= 1) ? c.bounds + ((i - 1) / 2) * kBoundsWords : nullptr;
         if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt,
-                             nxt ? tab : nullptr, nxt ? c.done : nullptr)))
+                             nxt ? tab : nullptr, nxt ? c.done : nullptr, cl)))
             return st;
         sk = dk;
         sv = dv;

@@ -106,6 +106,10 @@ struct ScatterArgs {
     // own, read by every workgroup before it finished) and re-arms *done (zero on entry)
     uint32_t *tail_zero;
     uint32_t *done;
+    // k = 8 line kernels: != nullptr -> launch_scatter launches the plain and the clustered-input
+    // variant (rank_add_hot); *cl_select == 0 (a pass whose digit groups were unbalanced: skewed,
+    // duplicate-heavy keys) runs the clustered one, anything else the plain one
+    const uint32_t *cl_select;
 };
 
 struct ScanArgs {

@@ -74,6 +74,36 @@ __device__ __forceinline__ void count_add(uint32_t *cnt, uint32_t d, uint32_t in
     if (lane_id() == (uint32_t)__builtin_ctzll(ma)) atomicAdd(&cnt[da], inc * (uint32_t)__popcll(ma));
 }
 
+// One returning add for all lanes of a wave: the lanes whose digit is c (mask m) are served by the
+// first of them, adding their count, and get base + their rank among m (mbcnt); every other lane
+// adds 1 (lane-ordered). One ds_add_rtn instruction.
+__device__ __forceinline__ uint32_t agg_add(uint32_t *cnt, uint32_t d, uint32_t c, uint64_t m) {
+    const uint32_t la = (uint32_t)__builtin_ctzll(m);
+    const bool mine = d == c;
+    uint32_t o = 0;
+    if (!mine || lane_id() == la) o = atomicAdd(&cnt[d], mine ? (uint32_t)__popcll(m) : 1u);
+    const uint32_t base = __builtin_amdgcn_readlane(o, la);
+    return mine ? base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) : o;
+}
+
+// rank_add for clustered input (the clustered-pass kernels, rs_scatter_lines<..., CL = 1>): when the
+// first lane's digit is not common, the wave's last aggregated digit (`hot`, wave-uniform) is the
+// second candidate -- a run of a hot key covers many consecutive slots, but where it holds ~2/3 of
+// a slot's lanes the first lane holds another key a third of the time, and then ~40 lanes would
+// serialise on one counter (dev/lines_exp.hip, Zipf pass 1: 2.35 -> 2.16 ms; it costs ~12 % on
+// unclustered input, so only the clustered kernels use it).
+__device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint32_t &hot) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t ma = __ballot(d == da);
+    if (__popcll(ma) >= 16) {
+        hot = da;
+        return agg_add(cnt, d, da, ma);
+    }
+    const uint64_t mh = __ballot(d == hot);
+    if (__popcll(mh) >= 8) return agg_add(cnt, d, hot, mh);
+    return atomicAdd(&cnt[d], 1u);
+}
+
 // Value of lane (first lane of this lane's aligned group of TPD lanes) + q, for q < TPD: DPP
 // quad permutes (one VALU, no LDS) for groups of up to 4 lanes, ds_bpermute otherwise.
 template <uint32_t TPD>
@@ -837,7 +867,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0>
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -882,6 +912,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     uint64_t cend = min(cbeg + a.chunk_keys, a.n);
     uint32_t head = 0;  // leading keys of the first tile that belong to the previous chunk
+    // clustered-pass selection (ScatterArgs::cl_select): the plain and the clustered kernel are both
+    // launched, and the one not selected by the device-side flag leaves at once
+    if (a.cl_select != nullptr && ((*a.cl_select == 0u) != (CL != 0))) return;
     if (a.bounds != nullptr && a.bounds[0] != 0u) {
         // digit-group chunk (rs_histogram_joint): any start, so the tiles start at the 256-B
         // boundary below it (every wave load stays two whole 128-B lines), the first tile skips
@@ -1010,6 +1043,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
+    uint32_t hotd = 0xFFFFFFFFu;  // CL: the wave's last aggregated digit (none yet)
 
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
@@ -1040,7 +1074,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
                 const uint32_t dj = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                const uint32_t r = rank_add(&s_cnt[w * R], dj);
+                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * R], dj, hotd) : rank_add(&s_cnt[w * R], dj);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
@@ -1612,9 +1646,21 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
         fn = bits == 3 ? reinterpret_cast<void *>(&rs_scatter_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>)
                        : reinterpret_cast<void *>(&rs_scatter_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>);
     }
+    // clustered-input variants of the k = 8 line kernels (rank_add_hot): both kernels are launched,
+    // the device-side flag *cl_select picks the one that works (the other leaves at once: ~3 us)
+    void *cl = nullptr;
+    if (a.cl_select != nullptr) {
+        if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3>))
+            cl = reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>);
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2>))
+            cl = reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>);
+    }
     ScatterArgs copy = a;
+    if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
     void *args[] = {&copy};
-    return hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
+    hipError_t e = hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
+    if (e != hipSuccess || cl == nullptr) return e;
+    return hipLaunchKernel(cl, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
 }
 
 int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmode) {

@@ -21,6 +21,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 
 #include <vector>
@@ -55,7 +56,58 @@ using namespace rsort;
 #define LX_FLUSH()
 #endif
 
-enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64 };
+enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
+       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096 };
+
+// one returning add for the lanes whose digit is c (by the first of them, adding their count)
+// and every other lane (adding 1): ONE ds_add_rtn instruction; ranks of c's lanes from mbcnt
+__device__ __forceinline__ uint32_t agg_add(uint32_t *cnt, uint32_t d, uint32_t c, uint64_t m) {
+    const uint32_t la = (uint32_t)__builtin_ctzll(m);
+    const bool mine = d == c;
+    uint32_t o = 0;
+    if (!mine || lane_id() == la) o = atomicAdd(&cnt[d], mine ? (uint32_t)__popcll(m) : 1u);
+    const uint32_t base = __builtin_amdgcn_readlane(o, la);
+    return mine ? base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) : o;
+}
+
+// kHot2: first-lane candidate, then the wave's last aggregated digit (runs of a hot key span slots)
+__device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint32_t &hot) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t ma = __ballot(d == da);
+    if (__popcll(ma) >= 16) {
+        hot = da;
+        return agg_add(cnt, d, da, ma);
+    }
+    const uint64_t mh = __ballot(d == hot);
+    if (__popcll(mh) >= 8) return agg_add(cnt, d, hot, mh);
+    return atomicAdd(&cnt[d], 1u);
+}
+
+// kRuns: runs of equal digits on consecutive lanes (every 16-lane row starts a run) -- only each
+// run's first lane adds, the run's length; its lanes take base + offset (a DPP max scan per row)
+template <bool AGG>
+__device__ __forceinline__ uint32_t rank_runs(uint32_t *cnt, uint32_t d) {
+    if constexpr (AGG) {
+        const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+        const uint64_t ma = __ballot(d == da);
+        if (__popcll(ma) >= 16) return agg_add(cnt, d, da, ma);
+    }
+    const uint32_t dp = (uint32_t)__builtin_amdgcn_update_dpp((int)~d, (int)d, 0x111, 0xf, 0xf, false);  // row_shr:1
+    const bool head = dp != d;
+    const uint64_t H = __ballot(head);
+    if (__popcll(H) > 40) return atomicAdd(&cnt[d], 1u);
+    const uint32_t lane = lane_id();
+    const uint64_t above = H & ~((2ull << lane) - 1ull);
+    const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+    uint32_t o = 0;
+    if (head) o = atomicAdd(&cnt[d], next - lane);
+    uint32_t v = head ? ((lane << 16) | o) : 0u;
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    return (v & 0xFFFFu) + lane - (v >> 16);
+}
 
 template <int BITS, int THREADS, int KPT, int G, int V>
 __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
@@ -101,6 +153,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
     }
     if (t < 2) s_clust[t] = 0;
     uint32_t clustered = 1;  // RANK1: the first tile checks
+    uint32_t hotd = 0xFFFFFFFFu;  // HOT2: the wave's last aggregated digit
     uint32_t par = 0;
 
     const uint32_t base = w * SEG + lane;
@@ -163,11 +216,38 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
                     const uint32_t r = atomicAdd(&s_cnt[w * R + dj], 1u);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
+            } else if ((V & kGateW) && __builtin_expect([&] {
+                           // this wave's tile is clustered: runs of equal digits on consecutive lanes
+                           // in slots 0 and KPT / 2 (uniform keys: 1 lane in 256 matches its neighbour)
+                           const uint32_t a0 = dig(key[0]), a1 = dig(key[KPT / 2]);
+                           const uint32_t p0 = (uint32_t)__builtin_amdgcn_update_dpp((int)~a0, (int)a0, 0x111, 0xf, 0xf, false);
+                           const uint32_t p1 = (uint32_t)__builtin_amdgcn_update_dpp((int)~a1, (int)a1, 0x111, 0xf, 0xf, false);
+                           return __popcll(__ballot(p0 == a0)) + __popcll(__ballot(p1 == a1)) >= 16;
+                       }(), 0)) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t dj = dig(key[j]);
+                    const uint32_t r = rank_add_hot(&s_cnt[w * R], dj, hotd);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            } else if ((V & kGate) && __builtin_expect(clustered != 0, 0)) {
+                // clustered tiles (the previous tile had a per-wave digit count >= 32 / 128): a
+                // second aggregation candidate, the wave's last aggregated digit
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t dj = dig(key[j]);
+                    const uint32_t r = rank_add_hot(&s_cnt[w * R], dj, hotd);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = rank_add(&s_cnt[w * R], dj);
+                    uint32_t r;
+                    if constexpr ((V & kHot2) != 0) r = rank_add_hot(&s_cnt[w * R], dj, hotd);
+                    else if constexpr ((V & kRuns) != 0) r = rank_runs<false>(&s_cnt[w * R], dj);
+                    else if constexpr ((V & kRunsAgg) != 0) r = rank_runs<true>(&s_cnt[w * R], dj);
+                    else r = rank_add(&s_cnt[w * R], dj);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
@@ -194,10 +274,10 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
                 const uint32_t v = sub * WPT + i;
                 wx[i] = v < (uint32_t)W ? s_cnt[v * R + d_own] : 0u;
                 part += wx[i];
-                hot |= wx[i] >= 32u;
+                hot |= wx[i] >= ((V & kGate128) ? 128u : 32u);
             }
         }
-        if constexpr ((V & kRank1) != 0) {
+        if constexpr ((V & (kRank1 | kGate)) != 0) {
             // slot par: set by any wave that saw a hot per-wave digit count, read after the barrier
             // below; slot par ^ 1 is reset for the next tile (its readers are a barrier behind)
             if (__ballot(hot) != 0 && lane == 0) s_clust[par] = 1;
@@ -269,7 +349,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
         }
         LX(3);
         __syncthreads();
-        if constexpr ((V & kRank1) != 0) {
+        if constexpr ((V & (kRank1 | kGate)) != 0) {
             clustered = s_clust[par];
             par ^= 1u;
         }
@@ -370,6 +450,7 @@ struct Ctx {
 };
 
 static const char *g_filter = nullptr;
+static int g_shift = 0;
 
 template <int BITS, int THREADS, int KPT, typename K>
 void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
@@ -438,6 +519,18 @@ void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
     printf("    cycles per tile (wave 0):");
     for (int i = 0; i < 7; ++i) printf(" %s=%.0f", names[i], sum[i] / chunks / tpc);
     printf("\n");
+    // the slowest chunk sets the kernel time (one workgroup per CU, all resident at once)
+    uint64_t worst = 0;
+    double wt = 0;
+    for (uint64_t b = 0; b < chunks; ++b) {
+        double tot = 0;
+        for (int i = 0; i < 7; ++i) tot += st[b * 8 + i];
+        if (tot > wt) { wt = tot; worst = b; }
+    }
+    printf("    slowest chunk %llu (%.2fx the mean):", (unsigned long long)worst,
+           wt / ((sum[0] + sum[1] + sum[2] + sum[3] + sum[4] + sum[5] + sum[6]) / chunks));
+    for (int i = 0; i < 7; ++i) printf(" %s=%.0f", names[i], (double)st[worst * 8 + i] / tpc);
+    printf("\n");
 #endif
     fflush(stdout);
 }
@@ -457,16 +550,54 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&c.stamps, 65536 * 8 * 8));
     CK(hipEventCreate(&c.e0));
     CK(hipEventCreate(&c.e1));
-    CK(launch_gen_uniform(c.keys, c.n, 0x5EED, 0));
+    const bool zipf = getenv("LX_ZIPF") != nullptr;
+    if (zipf) {
+        // Zipf(1.0) over 2^20 ranks, key = fmix32(rank) (bench.py --dist zipf, tests/_util.py)
+        const int ranks = 1 << 20;
+        std::vector<double> cum(ranks);
+        double acc = 0;
+        for (int r = 0; r < ranks; ++r) cum[r] = (acc += 1.0 / (r + 1.0));
+        std::vector<uint32_t> cdf(ranks);
+        for (int r = 0; r < ranks; ++r) {
+            const double t = floor(cum[r] / acc * 4294967296.0);
+            cdf[r] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+        }
+        cdf[ranks - 1] = 0xFFFFFFFFu;
+        uint32_t *d_cdf = nullptr;
+        CK(hipMalloc(&d_cdf, ranks * 4));
+        CK(hipMemcpy(d_cdf, cdf.data(), ranks * 4, hipMemcpyHostToDevice));
+        CK(launch_gen_zipf(c.keys, c.n, 0x5EED, d_cdf, ranks, 0));
+    } else {
+        CK(launch_gen_uniform(c.keys, c.n, 0x5EED, 0));
+    }
     CK(hipDeviceSynchronize());
-    printf("n=%llu cus=%d\n", (unsigned long long)c.n, c.cus);
+    // LX_PASS=p: the input of pass p of a sort (p library passes over fixed chunks first)
+    const int npre = getenv("LX_PASS") ? atoi(getenv("LX_PASS")) : 0;
+    for (int i = 0; i < npre; ++i) {
+        HistArgs h{};
+        h.keys = c.keys; h.table = c.table; h.n = c.n; h.chunk_keys = c.n / 256; h.num_chunks = 256;
+        h.shift = 8 * i; h.vec = 1; h.split = 1;
+        CK(launch_histogram(8, kDigitShift, h, 0));
+        ScanArgs sa{};
+        sa.table = c.table; sa.block_sums = c.bsums; sa.m = 256 * 256; sa.nblocks = (uint32_t)((sa.m + kScanSegment - 1) / kScanSegment);
+        CK(launch_scan(sa, 0));
+        ScatterArgs a{};
+        a.kin = c.keys; a.kout = c.out; a.table = c.table; a.n = c.n; a.chunk_keys = c.n / 256; a.num_chunks = 256;
+        a.shift = 8 * i;
+        rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3><<<256, 1024>>>(a);
+        CK(hipMemcpy(c.keys, c.out, c.n * 4, hipMemcpyDeviceToDevice));
+    }
+    g_shift = 8 * npre;
+    CK(hipDeviceSynchronize());
+    printf("n=%llu cus=%d keys=%s pass=%d\n", (unsigned long long)c.n, c.cus, zipf ? "zipf" : "uniform", npre);
     constexpr int OC = kOutB2 | kCopy64;
     for (int rep = 0; rep < 2; ++rep) {
-        run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3>, 0);
-        run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, 0);
-        run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, 0);
-        run<8, 1024, 16>(c, "lx outb2+copy64+prio", lx_lines<8, 1024, 16, 32, OC | kPrio>, 0);
-        run<8, 1024, 16>(c, "lx outb2+copy64+sb4", lx_lines<8, 1024, 16, 32, OC | kSB4>, 0);
+        run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3>, g_shift);
+        run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, g_shift);
+        run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, g_shift);
+        run<8, 1024, 16>(c, "lx hot2", lx_lines<8, 1024, 16, 32, OC | kHot2>, g_shift);
+        run<8, 1024, 16>(c, "lx gatew", lx_lines<8, 1024, 16, 32, OC | kGateW>, g_shift);
+        run<8, 1024, 16>(c, "lx gate128", lx_lines<8, 1024, 16, 32, OC | kGate | kGate128>, g_shift);
     }
     return 0;
 }

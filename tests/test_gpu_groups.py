@@ -102,6 +102,35 @@ def test_pass1_balanced_pass3_not():
     assert np.array_equal(y, oracle_sort(x, 8))
 
 
+@pytest.mark.parametrize("pairs", [False, True])
+def test_clustered_kernels(pairs):
+    """Unbalanced groups select the clustered-input kernels (rank_add_hot) for passes 1..3. Input
+    built to exercise both aggregation candidates: blocks where one hot key holds 40-95 % of the
+    positions (the first lane of a slot often holds another key, the wave's last aggregated digit
+    is then the candidate), hot keys that change between blocks, and background keys."""
+    tile = PAIRS_TILE if pairs else LINE_TILE
+    n = 768 * tile - 11
+    rng = np.random.default_rng(17)
+    x = uniform_keys(n, seed=17)
+    hot = rng.integers(0, 1 << 32, 64, dtype=np.uint64).astype(np.uint32)
+    blk = 3000
+    for b in range(0, n, blk):
+        h = hot[rng.integers(0, 64)]
+        dens = rng.uniform(0.4, 0.95)
+        m = rng.random(min(blk, n - b)) < dens
+        x[b:b + m.size][m] = h
+    # one heavy key overall: the digit groups are unbalanced, so the clustered kernels run
+    x[rng.random(n) < 0.1] = hot[0]
+    v = np.arange(n, dtype=np.uint32) if pairs else None
+    out, flags = run(x, group_plan(n, pairs=pairs), vals=v)
+    assert flags == [0, 0]
+    if pairs:
+        wk, wv = oracle_sort_pairs(x, v, 8)
+        assert np.array_equal(out[0], wk) and np.array_equal(out[1], wv)
+    else:
+        assert np.array_equal(out, oracle_sort(x, 8))
+
+
 @pytest.mark.parametrize("dist", ["uniform", "zipf"])
 def test_pairs_on_groups(dist):
     n = 768 * PAIRS_TILE - 9
