@@ -57,8 +57,16 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
              for v in vs if v * 1024.0 > 0.25 * 2.0 * n]
     hist_fetch = sum(hvals) / len(hvals) if hvals else None
     gen_write, _ = per_launch(write, "WRITE_SIZE", "rs_gen_uniform" if dist == "uniform" else "rs_gen_zipf")
-    sc_fetch, nf = per_launch(fetch, "FETCH_SIZE", "rs_scatter")
-    sc_write, nw = per_launch(write, "WRITE_SIZE", "rs_scatter")
+    # scatter launches that did the pass: the k = 8 kernels come as a plain and a clustered-input
+    # variant, both launched, the one not selected on the device leaving at once (bytes ~ 0)
+    algo_b = (16.0 if pairs else 8.0) * n
+
+    def working(agg, counter, frac):
+        vals = [v for (kn, c), vs in agg.items() if c == counter and "rs_scatter" in kn for v in vs
+                if v * 1024.0 > 0.01 * algo_b * frac]
+        return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+    sc_fetch, nf = working(fetch, "FETCH_SIZE", 0.25)   # FETCH_SIZE reports about half the read bytes
+    sc_write, nw = working(write, "WRITE_SIZE", 0.5)
     kib = 1024.0
     fetch_ratio = (hist_fetch * kib) / (4.0 * n) if hist_fetch else 0.5
     write_ratio = (gen_write * kib) / (4.0 * n) if gen_write else 1.0
@@ -73,10 +81,20 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
         rows[kn]["launches_" + c] = len(vs)
     # the rocprofv3 --stats average duration of the same scatter kernel (bench.py reports the
     # roofline fraction from it next to its own HIP-event figure)
+    # average over the launches that did the pass, from the same run's kernel trace (the --stats
+    # rows average each symbol over all its launches, the exits of the unselected variant included)
     rp_avg, rp_calls = None, 0
-    for r in csv.DictReader(open(stats)):
-        if r["Name"] in names or (not names and "rs_scatter" in r["Name"]):
-            rp_avg, rp_calls = float(r["AverageNs"]), int(r["Calls"])
+    trace = _one(src / "trace", "*kernel_trace.csv")
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+            if "rs_scatter" in r["Kernel_Name"]]
+    if durs:
+        work = [d for d in durs if d > 0.1 * max(durs)]
+        # the timed steps only (the first sorts of a process run on cold pages and clocks): the last
+        # steps x passes working launches, as bench.py's own line (same run) reports them
+        line = next((json.loads(x) for x in open(src / "bench_trace.log") if x.startswith("{")), None)
+        if line:
+            work = work[-int(line["steps"]) * int(line["config"]["passes"]):]
+        rp_avg, rp_calls = sum(work) / len(work), len(work)
     path = HERE / f"{tag}_pmc.json"
     prev = json.loads(path.read_text()) if path.exists() else {}
     cfg = f"n{n}_k{k}_{dist}_{'pairs' if pairs else 'keys'}_match:{kernel}"
@@ -102,7 +120,8 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
                 "calibration": {"fetch_ratio": round(fetch_ratio, 4), "write_ratio": round(write_ratio, 4)},
                 "rocprof_avg_ns": rp_avg,
                 "rocprof_calls": rp_calls,
-                "rocprof_source": f"profiles/{stats_tag or tag}_kernel_stats.csv",
+                "rocprof_source": f"profiles/{stats_tag or tag}_kernel_stats.csv (per-symbol totals); the average "
+                                  f"is over the working launches of the same run's kernel trace",
             }
         },
         "per_kernel_raw": {**prev.get("per_kernel_raw", {}), cfg: rows},
