@@ -59,29 +59,7 @@ using namespace rsort;
 enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
        kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096 };
 
-// one returning add for the lanes whose digit is c (by the first of them, adding their count)
-// and every other lane (adding 1): ONE ds_add_rtn instruction; ranks of c's lanes from mbcnt
-__device__ __forceinline__ uint32_t agg_add(uint32_t *cnt, uint32_t d, uint32_t c, uint64_t m) {
-    const uint32_t la = (uint32_t)__builtin_ctzll(m);
-    const bool mine = d == c;
-    uint32_t o = 0;
-    if (!mine || lane_id() == la) o = atomicAdd(&cnt[d], mine ? (uint32_t)__popcll(m) : 1u);
-    const uint32_t base = __builtin_amdgcn_readlane(o, la);
-    return mine ? base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) : o;
-}
-
-// kHot2: first-lane candidate, then the wave's last aggregated digit (runs of a hot key span slots)
-__device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint32_t &hot) {
-    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
-    const uint64_t ma = __ballot(d == da);
-    if (__popcll(ma) >= 16) {
-        hot = da;
-        return agg_add(cnt, d, da, ma);
-    }
-    const uint64_t mh = __ballot(d == hot);
-    if (__popcll(mh) >= 8) return agg_add(cnt, d, hot, mh);
-    return atomicAdd(&cnt[d], 1u);
-}
+// agg_add and rank_add_hot (kHot2) are the library's (rsort_kernels.hip)
 
 // kRuns: runs of equal digits on consecutive lanes (every 16-lane row starts a run) -- only each
 // run's first lane adds, the run's length; its lanes take base + offset (a DPP max scan per row)
@@ -138,6 +116,12 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
     uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     uint64_t cend = min(cbeg + a.chunk_keys, a.n);
     uint32_t head = 0;
+    if (a.bounds != nullptr && a.bounds[0] != 0u) {  // digit-group chunks (as the library kernel)
+        const uint64_t b = a.bounds[1 + c];
+        cend = a.bounds[2 + c];
+        cbeg = b < cend ? (b & ~(uint64_t)(kWave - 1)) : cend;
+        head = (uint32_t)(b < cend ? b - cbeg : 0);
+    }
 
     const uint32_t d_own = t / TPD;
     const uint32_t sub = t % TPD;
@@ -433,6 +417,14 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
     LX_FLUSH();
 }
 
+// reads every stride-th word of buf (keeps a sum so the loads stay)
+__global__ void touch(const uint32_t *buf, uint64_t n, uint64_t stride, unsigned long long *sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * stride; i < n; i += (uint64_t)gridDim.x * blockDim.x * stride)
+        acc += buf[i];
+    if (acc == 0x12345678u) atomicAdd(sink, 1ull);
+}
+
 __global__ void count_mismatch(const uint32_t *a, const uint32_t *b, uint64_t n, unsigned long long *bad) {
     unsigned long long local = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -442,7 +434,8 @@ __global__ void count_mismatch(const uint32_t *a, const uint32_t *b, uint64_t n,
 
 struct Ctx {
     uint64_t n;
-    uint32_t *keys, *out, *ref, *table, *bsums;
+    uint32_t *keys, *out, *ref, *table, *bsums, *joint, *bounds;
+    bool groups = false;  // LX_GROUPS=1 (with LX_PASS=1): pass 1 on the digit-0 groups
     unsigned long long *bad, *stamps;
     int cus;
     hipEvent_t e0, e1;
@@ -451,6 +444,7 @@ struct Ctx {
 
 static const char *g_filter = nullptr;
 static int g_shift = 0;
+static int g_disturb = 0;
 
 template <int BITS, int THREADS, int KPT, typename K>
 void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
@@ -471,6 +465,10 @@ void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
     h.shift = shift;
     h.vec = 1;
     h.split = 1;
+    if (c.groups) {  // the table is the joint counts (copy mode), the chunks the groups
+        h.bounds = c.bounds;
+        h.copy_src = c.joint;
+    }
     CK(launch_histogram(BITS, kDigitShift, h, 0));
     ScanArgs s{};
     s.table = c.table;
@@ -487,17 +485,35 @@ void run(Ctx &c, const char *name, K kern, int shift, int reps = 10) {
     a.num_chunks = (uint32_t)chunks;
     a.shift = shift;
     a.stamps = c.stamps;
+    if (c.groups) a.bounds = c.bounds;
     CK(hipMemset(c.out, 0, c.n * 4));
     kern<<<chunks, THREADS>>>(a);
     CK(hipDeviceSynchronize());
-    CK(hipEventRecord(c.e0, 0));
-    for (int i = 0; i < reps; ++i) kern<<<chunks, THREADS>>>(a);
-    CK(hipEventRecord(c.e1, 0));
-    CK(hipEventSynchronize(c.e1));
-    CK(hipGetLastError());
     float ms = 0;
-    CK(hipEventElapsedTime(&ms, c.e0, c.e1));
-    ms /= reps;
+    if (g_disturb == 0) {
+        CK(hipEventRecord(c.e0, 0));
+        for (int i = 0; i < reps; ++i) kern<<<chunks, THREADS>>>(a);
+        CK(hipEventRecord(c.e1, 0));
+        CK(hipEventSynchronize(c.e1));
+        CK(hipGetLastError());
+        CK(hipEventElapsedTime(&ms, c.e0, c.e1));
+        ms /= reps;
+    } else {
+        // LX_DISTURB: before each timed launch, read another 4 GiB buffer (caches and TLBs hold
+        // other data), then 2: touch one word per 64 KiB of the input, 3: read the whole input
+        for (int i = 0; i < reps; ++i) {
+            touch<<<4096, 256>>>(c.ref, c.n, 1, c.bad + 1);
+            if (g_disturb == 2) touch<<<4096, 256>>>(c.keys, c.n, 16384, c.bad + 1);
+            if (g_disturb == 3) touch<<<4096, 256>>>(c.keys, c.n, 1, c.bad + 1);
+            CK(hipEventRecord(c.e0, 0));
+            kern<<<chunks, THREADS>>>(a);
+            CK(hipEventRecord(c.e1, 0));
+            CK(hipEventSynchronize(c.e1));
+            float one = 0;
+            CK(hipEventElapsedTime(&one, c.e0, c.e1));
+            ms += one / reps;
+        }
+    }
     unsigned long long bad = 0;
     if (!c.have_ref) {
         CK(hipMemcpy(c.ref, c.out, c.n * 4, hipMemcpyDeviceToDevice));
@@ -546,7 +562,7 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&c.ref, c.n * 4));
     CK(hipMalloc(&c.table, (c.n / 1024 + 65536) * 4 * 16));
     CK(hipMalloc(&c.bsums, 1 << 24));
-    CK(hipMalloc(&c.bad, 8));
+    CK(hipMalloc(&c.bad, 16));
     CK(hipMalloc(&c.stamps, 65536 * 8 * 8));
     CK(hipEventCreate(&c.e0));
     CK(hipEventCreate(&c.e1));
@@ -573,6 +589,19 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
     // LX_PASS=p: the input of pass p of a sort (p library passes over fixed chunks first)
     const int npre = getenv("LX_PASS") ? atoi(getenv("LX_PASS")) : 0;
+    g_disturb = getenv("LX_DISTURB") ? atoi(getenv("LX_DISTURB")) : 0;
+    CK(hipMalloc(&c.joint, 65536 * 4));
+    CK(hipMalloc(&c.bounds, 1024 * 4));
+    if (getenv("LX_GROUPS") && npre == 1) {
+        // joint counts (digit 0, digit 1) of the input and the digit-0 group bounds (library kernels)
+        CK(hipMemset(c.joint, 0, 65536 * 4));
+        HistArgs hj{};
+        hj.keys = c.keys; hj.table = c.table; hj.n = c.n; hj.chunk_keys = c.n / 256; hj.num_chunks = 256;
+        hj.shift = 0; hj.vec = 1; hj.split = 1; hj.joint = c.joint;
+        CK(launch_histogram_joint(hj, 0));
+        CK(launch_joint_bounds(c.joint, nullptr, c.bounds, c.n, c.n / 256 + 16384, 0));
+        c.groups = true;
+    }
     for (int i = 0; i < npre; ++i) {
         HistArgs h{};
         h.keys = c.keys; h.table = c.table; h.n = c.n; h.chunk_keys = c.n / 256; h.num_chunks = 256;
@@ -589,7 +618,8 @@ int main(int argc, char **argv) {
     }
     g_shift = 8 * npre;
     CK(hipDeviceSynchronize());
-    printf("n=%llu cus=%d keys=%s pass=%d\n", (unsigned long long)c.n, c.cus, zipf ? "zipf" : "uniform", npre);
+    printf("n=%llu cus=%d keys=%s pass=%d%s\n", (unsigned long long)c.n, c.cus, zipf ? "zipf" : "uniform", npre,
+           c.groups ? " groups" : "");
     constexpr int OC = kOutB2 | kCopy64;
     for (int rep = 0; rep < 2; ++rep) {
         run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3>, g_shift);
