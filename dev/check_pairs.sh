@@ -1,8 +1,10 @@
-# dev/check_pairs.sh -- pairs GPU tests, then the pairs benches (C4 and uniform pairs)
+# dev/check_pairs.sh -- one gpurun call: pairs parity (dense 128-B-line pairs kernel), then bench
+# lines of uniform pairs and C4, and a kernel trace of C4
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "pairs or partition or multi or groups" > gpurun_out/pairs_tests.log 2>&1
-timeout -k 10 180 python bench.py --no-cpu --dist zipf --pairs > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err
-timeout -k 10 180 python bench.py --no-cpu --pairs > gpurun_out/bench_upairs.json 2> gpurun_out/bench_upairs.err
-timeout -k 10 180 python bench.py --no-cpu > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err
+timeout -k 10 400 python -u -m pytest tests/test_gpu_groups.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "pairs or clustered" > gpurun_out/pairs_tests.log 2>&1
+timeout -k 10 200 python bench.py --no-cpu --no-e2e --pairs > gpurun_out/pairs_u.json 2> gpurun_out/pairs_u.err
+timeout -k 10 200 python bench.py --no-cpu --no-e2e --pairs --dist zipf > gpurun_out/pairs_c4.json 2> gpurun_out/pairs_c4.err
+bash dev/kt.sh c4p --pairs --dist zipf
+bash dev/kt.sh up --pairs

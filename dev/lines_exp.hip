@@ -623,6 +623,7 @@ int main(int argc, char **argv) {
     constexpr int OC = kOutB2 | kCopy64;
     for (int rep = 0; rep < 2; ++rep) {
         run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3>, g_shift);
+        run<8, 1024, 16>(c, "lib G16 (64-B lines)", rs_scatter_lines<8, 1024, 16, 16, false, kDigitShift, 3>, g_shift);
         run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, g_shift);
         run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, g_shift);
         run<8, 1024, 16>(c, "lx hot2", lx_lines<8, 1024, 16, 32, OC | kHot2>, g_shift);

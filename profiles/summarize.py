@@ -74,7 +74,7 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
     write_bytes = sc_write * kib / write_ratio
     algo = (16.0 if pairs else 8.0) * n
     names = {kn for (kn, c) in list(fetch) + list(write) if "rs_scatter" in kn}
-    kernel = "rs_scatter_lines" if any("rs_scatter_lines" in kn for kn in names) else "rs_scatter"
+    kernel = next((k for k in ("rs_scatter_pairs", "rs_scatter_lines") if any(k in kn for kn in names)), "rs_scatter")
     rows = {}
     for (kn, c), vs in sorted(fetch.items()) + sorted(write.items()):
         rows.setdefault(kn, {})[c + "_KiB_per_launch"] = sum(vs) / len(vs)
