@@ -104,6 +104,20 @@ __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint
     return atomicAdd(&cnt[d], 1u);
 }
 
+// Row stride of per-wave digit counters [wave][digit] read column-wise by digit groups: TPD threads
+// per digit, thread `sub` taking rows sub * WPT .. + WPT - 1. With rows R apart (R a multiple of
+// 64) the TPD threads of a digit hit one bank; a stride with WPT * RS = 64 / TPD (mod 64) puts the
+// 64 / TPD digits x TPD threads of a wave on 64 different banks (k = 8, 1024 threads: 260;
+// dev/lines_exp.hip "lx pad": step 2 2.1K -> 1.75K cycles per tile, C3 pass -1.5 %). Groups wider
+// than the wave count (WPT = 0 here) read one row per thread and keep R.
+template <uint32_t R, uint32_t TPD, uint32_t WPT>
+constexpr uint32_t counter_stride() {
+    if (TPD < 2 || WPT == 0 || 64 % TPD != 0) return R;
+    for (uint32_t p = 0; p < 64; ++p)
+        if (((R + p) * WPT) % 64 == (64 / TPD) % 64) return R + p;
+    return R;
+}
+
 // Value of lane (first lane of this lane's aligned group of TPD lanes) + q, for q < TPD: DPP
 // quad permutes (one VALU, no LDS) for groups of up to 4 lanes, ds_bpermute otherwise.
 template <uint32_t TPD>
@@ -885,7 +899,10 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     // staging: [0, CAP) whole lines of every digit, [CAP, CAP + R*G) the per-digit carries
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];  // + padding sink
     __shared__ __attribute__((aligned(16))) uint32_t s_vstage[PAIRS ? CAP + R * G + 4 : 4];
-    __shared__ uint32_t s_cnt[W * R + 1];                                        // + padding counter
+    // per-wave counter rows RS >= R words apart (counter_stride): step 2's digit-group threads read
+    // and write rows sub * WPT + i of their digit's column, which R apart share one bank
+    constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
+    __shared__ uint32_t s_cnt[W * RS + 1];                                       // + padding counter
     __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
@@ -1056,7 +1073,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         head = 0;
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
-        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
         // rank first: the returning add IS the key's rank among its wave's keys of that digit
         // (lane order, kRankAtomic); two ranks (< 2^16) per register
         uint32_t rk[(KPT + 1) / 2];
@@ -1074,7 +1091,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
                 const uint32_t dj = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * R], dj, hotd) : rank_add(&s_cnt[w * R], dj);
+                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
@@ -1083,7 +1100,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 const uint32_t d = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= d << (4 * (j % 8));
                 uint32_t r = 0;
-                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         }
@@ -1100,7 +1117,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 #pragma unroll
             for (uint32_t i = 0; i < WPT; ++i) {
                 const uint32_t v = sub * WPT + i;
-                wx[i] = v < (uint32_t)W ? s_cnt[v * R + d_own] : 0u;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
                 part += wx[i];
             }
         }
@@ -1129,7 +1146,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                     if (v < (uint32_t)W) {
                         // {LDS base | the digit's line limit << 16} (both < CAP < 2^16), read back
                         // with one ds_read_b32 per key in step 3
-                        s_cnt[v * R + d] = acc | ((gS + gw) << 16);
+                        s_cnt[v * RS + d] = acc | ((gS + gw) << 16);
                     }
                     acc += wx[i];
                 }
@@ -1207,7 +1224,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 asm volatile("" : "+v"(key[j]));  // recompute: CSE with step 1 would pin KPT digits
                 if constexpr (PD) dd[u] = (dpk[j / 8] >> (4 * (j % 8))) & 15u;
                 else dd[u] = dig(key[j]);
-                const uint32_t bl = s_cnt[w * R + dd[u]];
+                const uint32_t bl = s_cnt[w * RS + dd[u]];
                 pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
                 ll[u] = bl >> 16;
             }

@@ -57,7 +57,7 @@ using namespace rsort;
 #endif
 
 enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
-       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096 };
+       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384 };
 
 // agg_add and rank_add_hot (kHot2) are the library's (rsort_kernels.hip)
 
@@ -102,7 +102,10 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
     static_assert(R <= THREADS && TPD <= kWave && (G == 16 || G == 32), "geometry");
 
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[CAP + R * G + 4];
-    __shared__ uint32_t s_cnt[W * R + 1];
+    // kPad: per-wave counter rows R + 4 words apart, so the digit-group threads of step 2 (TPD = 4
+    // threads per digit, rows 4 sub + i) hit 64 different banks (R apart they hit 16, 4-way)
+    constexpr uint32_t RS = (V & kPad) ? R + 4 : R;
+    __shared__ uint32_t s_cnt[W * RS + 1];
     __shared__ uint2 s_out[R];
     __shared__ uint2 s_flush[R];
     __shared__ uint32_t s_ws[W];
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
         head = 0;
         LX(0);
 #pragma unroll
-        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
         uint32_t rk[(KPT + 1) / 2];
         uint32_t nkey[KPT];
         if (full) {
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = atomicAdd(&s_cnt[w * R + dj], 1u);
+                    const uint32_t r = atomicAdd(&s_cnt[w * RS + dj], 1u);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             } else if ((V & kGateW) && __builtin_expect([&] {
@@ -211,7 +214,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = rank_add_hot(&s_cnt[w * R], dj, hotd);
+                    const uint32_t r = rank_add_hot(&s_cnt[w * RS], dj, hotd);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             } else if ((V & kGate) && __builtin_expect(clustered != 0, 0)) {
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = rank_add_hot(&s_cnt[w * R], dj, hotd);
+                    const uint32_t r = rank_add_hot(&s_cnt[w * RS], dj, hotd);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             } else {
@@ -228,10 +231,10 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
                     uint32_t r;
-                    if constexpr ((V & kHot2) != 0) r = rank_add_hot(&s_cnt[w * R], dj, hotd);
-                    else if constexpr ((V & kRuns) != 0) r = rank_runs<false>(&s_cnt[w * R], dj);
-                    else if constexpr ((V & kRunsAgg) != 0) r = rank_runs<true>(&s_cnt[w * R], dj);
-                    else r = rank_add(&s_cnt[w * R], dj);
+                    if constexpr ((V & kHot2) != 0) r = rank_add_hot(&s_cnt[w * RS], dj, hotd);
+                    else if constexpr ((V & kRuns) != 0) r = rank_runs<false>(&s_cnt[w * RS], dj);
+                    else if constexpr ((V & kRunsAgg) != 0) r = rank_runs<true>(&s_cnt[w * RS], dj);
+                    else r = rank_add(&s_cnt[w * RS], dj);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = dig(key[j]);
                 uint32_t r = 0;
-                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * R + d], 1u);
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         }
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
 #pragma unroll
             for (uint32_t i = 0; i < WPT; ++i) {
                 const uint32_t v = sub * WPT + i;
-                wx[i] = v < (uint32_t)W ? s_cnt[v * R + d_own] : 0u;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
                 part += wx[i];
                 hot |= wx[i] >= ((V & kGate128) ? 128u : 32u);
             }
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
 #pragma unroll
                 for (uint32_t i = 0; i < WPT; ++i) {
                     const uint32_t v = sub * WPT + i;
-                    if (v < (uint32_t)W) s_cnt[v * R + d] = acc | ((gS + gw) << 16);
+                    if (v < (uint32_t)W) s_cnt[v * RS + d] = acc | ((gS + gw) << 16);
                     acc += wx[i];
                 }
             }
@@ -295,7 +298,22 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
             static_assert(G % TPD == 0 && CB % 4 == 0, "quad carries");
             const uint32_t x0 = sub * CB;
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            if ((V & kCopy64) != 0 && gw > 0 && x0 < gc) {
+            if ((V & kCopyI) != 0) {
+                // interleaved dword copy: the group's lanes take consecutive slots (no bank conflicts)
+                if (gw > 0) {
+                    uint32_t ck[G / TPD];
+#pragma unroll
+                    for (uint32_t i = 0; i < G / TPD; ++i) {
+                        const uint32_t x = sub + i * TPD;
+                        ck[i] = s_stage[CAP + d * G + x];
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < G / TPD; ++i) {
+                        const uint32_t x = sub + i * TPD;
+                        if (x < gc) s_stage[gS + x] = ck[i];
+                    }
+                }
+            } else if ((V & kCopy64) != 0 && gw > 0 && x0 < gc) {
                 u32x2 ck[CB / 2];
 #pragma unroll
                 for (uint32_t i = 0; i < CB / 2; ++i)
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
                 const int j = j0 + u;
                 asm volatile("" : "+v"(key[j]));
                 dd[u] = dig(key[j]);
-                const uint32_t bl = s_cnt[w * R + dd[u]];
+                const uint32_t bl = s_cnt[w * RS + dd[u]];
                 pp[u] = (bl & 0xFFFFu) + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
                 ll[u] = bl >> 16;
             }
@@ -623,12 +641,11 @@ int main(int argc, char **argv) {
     constexpr int OC = kOutB2 | kCopy64;
     for (int rep = 0; rep < 2; ++rep) {
         run<8, 1024, 16>(c, "lib rs_scatter_lines<8,1024,16,32,nt>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3>, g_shift);
-        run<8, 1024, 16>(c, "lib G16 (64-B lines)", rs_scatter_lines<8, 1024, 16, 16, false, kDigitShift, 3>, g_shift);
         run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, g_shift);
         run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, g_shift);
-        run<8, 1024, 16>(c, "lx hot2", lx_lines<8, 1024, 16, 32, OC | kHot2>, g_shift);
-        run<8, 1024, 16>(c, "lx gatew", lx_lines<8, 1024, 16, 32, OC | kGateW>, g_shift);
-        run<8, 1024, 16>(c, "lx gate128", lx_lines<8, 1024, 16, 32, OC | kGate | kGate128>, g_shift);
+        run<8, 1024, 16>(c, "lx pad", lx_lines<8, 1024, 16, 32, OC | kPad>, g_shift);
+        run<8, 1024, 16>(c, "lx copyi", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyI>, g_shift);
+        run<8, 1024, 16>(c, "lx pad+copyi", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyI | kPad>, g_shift);
     }
     return 0;
 }
