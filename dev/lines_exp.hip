@@ -57,7 +57,7 @@ using namespace rsort;
 #endif
 
 enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
-       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384 };
+       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384, kCopyR = 32768 };
 
 // agg_add and rank_add_hot (kHot2) are the library's (rsort_kernels.hip)
 
@@ -298,7 +298,27 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
             static_assert(G % TPD == 0 && CB % 4 == 0, "quad carries");
             const uint32_t x0 = sub * CB;
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-            if ((V & kCopyI) != 0) {
+            if ((V & kCopyR) != 0) {
+                // 8-B units, each thread's 4 units rotated by the digit: the 16 digits of a wave
+                // then touch different banks (segment heads and carry areas sit at 0 or 32 mod 64)
+                typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+                constexpr uint32_t UPT = G / 2 / TPD;  // units per thread
+                if (gw > 0) {
+                    const uint32_t rot = d & (G / 2 - 1);
+                    u32x2 ck[UPT];
+#pragma unroll
+                    for (uint32_t i = 0; i < UPT; ++i) {
+                        const uint32_t u = (sub + TPD * i + rot) & (G / 2 - 1);
+                        ck[i] = *reinterpret_cast<const u32x2 *>(&s_stage[CAP + d * G + 2 * u]);
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < UPT; ++i) {
+                        const uint32_t x = 2 * ((sub + TPD * i + rot) & (G / 2 - 1));
+                        if (x + 2 <= gc) *reinterpret_cast<u32x2 *>(&s_stage[gS + x]) = ck[i];
+                        else if (x < gc) s_stage[gS + x] = ck[i][0];
+                    }
+                }
+            } else if ((V & kCopyI) != 0) {
                 // interleaved dword copy: the group's lanes take consecutive slots (no bank conflicts)
                 if (gw > 0) {
                     uint32_t ck[G / TPD];
@@ -644,8 +664,7 @@ int main(int argc, char **argv) {
         run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, g_shift);
         run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, g_shift);
         run<8, 1024, 16>(c, "lx pad", lx_lines<8, 1024, 16, 32, OC | kPad>, g_shift);
-        run<8, 1024, 16>(c, "lx copyi", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyI>, g_shift);
-        run<8, 1024, 16>(c, "lx pad+copyi", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyI | kPad>, g_shift);
+        run<8, 1024, 16>(c, "lx pad+copyr", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyR | kPad>, g_shift);
     }
     return 0;
 }
