@@ -1,7 +1,8 @@
 """dev/ktsum.py TAG [passes] -- scatter launches that did a pass (not the exiting clustered/plain
 twin) of the last 2 sorts in gpurun_out/kt_TAG, in order, and their per-pass means."""
 import csv, glob, sys
-f = glob.glob(f"gpurun_out/kt_{sys.argv[1]}/*/*kernel_trace.csv")[0]
+import os
+f = max(glob.glob(f"gpurun_out/kt_{sys.argv[1]}/*/*kernel_trace.csv"), key=os.path.getmtime)
 P = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if "rs_scatter" in r["Kernel_Name"]]

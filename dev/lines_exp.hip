@@ -57,7 +57,7 @@ using namespace rsort;
 #endif
 
 enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
-       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384, kCopyR = 32768 };
+       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384, kCopyR = 32768, kStSc1 = 65536, kStPlain = 131072, kStNtSc1 = 262144 };
 
 // agg_add and rank_add_hot (kHot2) are the library's (rsort_kernels.hip)
 
@@ -166,7 +166,17 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
         const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
         const uint64_t gp = (uint64_t)(info.x + L * G + q);
         if (lo <= q) {
-            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
+            u32x4 *dst = reinterpret_cast<u32x4 *>(a.kout + gp);
+            if constexpr ((V & kStSc1) != 0) {
+                // write-through: the line leaves L2 at once, in issue order
+                asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(kv) : "memory");
+            } else if constexpr ((V & kStNtSc1) != 0) {
+                asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(dst), "v"(kv) : "memory");
+            } else if constexpr ((V & kStPlain) != 0) {
+                *dst = kv;
+            } else {
+                __builtin_nontemporal_store(kv, dst);
+            }
         } else {
 #pragma unroll
             for (uint32_t x = 0; x < 4; ++x)
@@ -664,7 +674,9 @@ int main(int argc, char **argv) {
         run<8, 1024, 16>(c, "lx base", lx_lines<8, 1024, 16, 32, 0>, g_shift);
         run<8, 1024, 16>(c, "lx outb2+copy64", lx_lines<8, 1024, 16, 32, OC>, g_shift);
         run<8, 1024, 16>(c, "lx pad", lx_lines<8, 1024, 16, 32, OC | kPad>, g_shift);
-        run<8, 1024, 16>(c, "lx pad+copyr", lx_lines<8, 1024, 16, 32, kOutB2 | kCopyR | kPad>, g_shift);
+        run<8, 1024, 16>(c, "lx pad sc1", lx_lines<8, 1024, 16, 32, OC | kPad | kStSc1>, g_shift);
+        run<8, 1024, 16>(c, "lx pad nt sc1", lx_lines<8, 1024, 16, 32, OC | kPad | kStNtSc1>, g_shift);
+        run<8, 1024, 16>(c, "lx pad plain", lx_lines<8, 1024, 16, 32, OC | kPad | kStPlain>, g_shift);
     }
     return 0;
 }

@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #define CK(x)                                                                     \
     do {                                                                          \
         hipError_t e_ = (x);                                                      \
@@ -91,6 +93,20 @@ int main(int argc, char **argv) {
         snprintf(nm, sizeof nm, "copy 1024x4q grid=%d/CU", g);
         timeit(nm, [&] { copy<1024, 4><<<cus * g, 1024>>>((const u32x4 *)a, (u32x4 *)b, n / 4); });
     }
+    // 256 regions (a k = 8 pass) from 16384-, 24576- and 32768-key tiles: runs of 64, 96, 128 keys
+    auto regions256 = [&](auto qtag) {
+        constexpr int Q = decltype(qtag)::value;
+        constexpr int TH = 1024;
+        constexpr uint32_t T = TH * Q * 4;
+        const uint64_t tiles = n / T;
+        const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+        const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+        snprintf(nm, sizeof nm, "256 regions, %5u-key tiles: runs of %u keys", T, T / 256);
+        timeit(nm, [&] { runs<TH, Q><<<g, TH>>>((const u32x4 *)a, b, n, T / 256, tpc, 0); });
+    };
+    regions256(std::integral_constant<int, 4>{});
+    regions256(std::integral_constant<int, 6>{});
+    regions256(std::integral_constant<int, 8>{});
     for (uint32_t L : {32u, 64u, 128u}) {
         for (uint32_t skew : {0u, 16u, 8u, 4u}) {
             constexpr int TH = 1024, Q = 4;
