@@ -225,7 +225,8 @@ Carve carve(const rsort_plan &p, void *ws) {
 // this pass's table and the joint counts; then the group bounds of pass p + 1. enable: nullptr,
 // or the previous joint pass's flag (its groups were unbalanced: count no joint either).
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
-                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, hipStream_t s) {
+                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, hipStream_t s,
+                       bool zero_joint) {
     HistArgs a{};
     a.keys = keys;
     a.table = table;
@@ -238,7 +239,10 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     a.joint = joint;
     a.joint_enable = enable;
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
-    if (hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess) return RSORT_ERR_HIP;
+    // the first joint count of a sort clears the counts; a later one finds them cleared by the
+    // copy-mode histogram that used them (or, where that pass fell back, is disabled by `enable`)
+    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess)
+        return RSORT_ERR_HIP;
     if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
     // a group may take one tile more than a fixed chunk
     return hip_status(launch_joint_bounds(joint, enable, bounds, (uint64_t)p.n,
@@ -247,7 +251,7 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
 
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                  int dmode, const uint32_t *split, int nsplit, hipStream_t s,
-                 const uint32_t *bounds = nullptr, const uint32_t *copy_src = nullptr) {
+                 const uint32_t *bounds = nullptr, uint32_t *copy_src = nullptr) {
     HistArgs a{};
     a.bounds = bounds;
     a.copy_src = copy_src;
@@ -265,8 +269,14 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     const int cus = device_cus();
     const int64_t want = 4 * (int64_t)(cus > 0 ? cus : 256);  // 1024-thread workgroups (hist_bits)
     a.split = 1;
-    if (p.num_chunks < want && p.chunk_keys >= 8 * 4096)
+    if (bounds != nullptr) {
+        // a digit-group pass (256 chunks of one workgroup each): copies the joint counts, or counts
+        // one chunk per 1024-thread workgroup (as fast as split workgroups, 0.62 ms per 2^30 keys,
+        // and no table memset launch)
+        a.wide = 1;
+    } else if (p.num_chunks < want && p.chunk_keys >= 8 * 4096) {
         a.split = (uint32_t)std::min<int64_t>({(want + p.num_chunks - 1) / p.num_chunks, p.chunk_keys / 4096, 64});
+    }
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
     if (a.split > 1 && hipMemsetAsync(table, 0, (size_t)p.table_entries * 4, s) != hipSuccess) return RSORT_ERR_HIP;
     return hip_status(launch_histogram(p.k_bits, dmode, a, s));
@@ -382,7 +392,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
-                                         c.bounds + (i / 2) * kBoundsWords, s)))
+                                         c.bounds + (i / 2) * kBoundsWords, s, i == 0)))
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint))) {

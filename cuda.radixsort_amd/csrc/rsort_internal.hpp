@@ -71,9 +71,10 @@ struct HistArgs {
     uint32_t splitters[kMaxSplitters];
     // Digit-group chunks (kJointBits plans, see rs_histogram_joint). bounds != nullptr and
     // bounds[0] != 0: this pass's table is copy_src (the previous pass's joint counts), copied
-    // instead of counted.
+    // instead of counted, and copy_src is cleared as it is read (the next counting pass adds into it).
     const uint32_t *bounds;
-    const uint32_t *copy_src;
+    uint32_t *copy_src;
+    uint32_t wide;          // 1: 1024-thread workgroups also with split == 1 (one per chunk, no memset)
     // rs_histogram_joint only: the joint counts [next digit][digit] are added into `joint`
     // (zeroed); joint_enable == nullptr or *joint_enable != 0 turns the joint count on.
     uint32_t *joint;

@@ -363,8 +363,10 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     if (a.bounds != nullptr && a.bounds[0] != 0u) {
         // digit-group chunks: this pass's table is the previous pass's joint counts
         const uint64_t m = (uint64_t)R * a.num_chunks;
-        for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < m; i += (uint64_t)gridDim.x * THREADS)
+        for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < m; i += (uint64_t)gridDim.x * THREADS) {
             a.table[i] = a.copy_src[i];
+            a.copy_src[i] = 0u;  // the next joint count adds into it: no memset launch
+        }
         return;
     }
     if constexpr (JOINT) {
@@ -1420,7 +1422,7 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
         }
         return hipErrorInvalidValue;
     }
-    if (a.split > 1) {
+    if (a.split > 1 || a.wide) {
         // few long chunks split over workgroups: 1024-thread workgroups read fastest
         // (dev/scatter_lab.hip "hist": 6.0 TB/s vs 5.6 TB/s for 256 threads)
         // non-temporal 16-B loads: 6.8 TB/s vs 6.1 TB/s; 8 sub-counters per digit: clustered

@@ -1,0 +1,8 @@
+# dev/check_nomemset.sh -- one gpurun call: group/parity/fullsize tests, bench C3 + Zipf, C3 kernel trace
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_groups.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q --timeout 300 --timeout-method thread > gpurun_out/nm_tests.log 2>&1
+timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-vendor > gpurun_out/nm_c3.json 2> gpurun_out/nm_c3.err
+timeout -k 10 200 python bench.py --no-cpu --no-e2e --no-vendor --dist zipf > gpurun_out/nm_zipf.json 2> gpurun_out/nm_zipf.err
+bash dev/kt.sh nm
