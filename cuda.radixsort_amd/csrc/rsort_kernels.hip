@@ -490,16 +490,17 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 }
 
 // The same exclusive scan as the tail of a kernel whose workgroups ADD into `table` with agent-scope
-// atomics (m entries, a multiple of 4, 16-B aligned): every workgroup waits for its adds and bumps
-// *done; the one whose bump comes last scans the table alone -- each thread a contiguous run of
-// m / THREADS entries -- clears `zero` (m entries) and re-arms *done. Next-digit plans (k = 3, 4)
+// atomics (m entries, a multiple of 4, 16-B aligned, < 4 GiB): every workgroup waits for its adds and
+// bumps *done; the one whose bump comes last scans the table alone -- each thread a contiguous run
+// of m / THREADS entries -- clears `zero` (m entries) and re-arms *done. Next-digit plans (k = 3, 4)
 // scan every table after the first this way: one launch per pass instead of three (rs_scan_reduce
 // + rs_scan_down, each ~5 us at C2, and their launch gaps).
-// Visibility (MI355X_MICROARCH.md, inter-workgroup visibility): atomics are performed beyond the
-// XCD's L2 and drop the line from it, nothing reads the table before the last workgroup does, and
-// that workgroup reads it with sc1 loads behind an agent acquire. The producers need no release
-// fence: a `buffer_wbl2` per workgroup (what __threadfence() issues) wrote back the default-policy
-// output held in L2 once per workgroup and doubled the C2 pass time. All threads must call it.
+// Visibility (MI355X_MICROARCH.md, inter-workgroup visibility, the table's first row): the payload
+// is agent-scope atomics, performed beyond the XCD's L2 (they drop the line), every adding wave
+// waits for them before its workgroup's one counter add, the last adder learns it from the value
+// its add returns, and every load of the table is a 16-B sc1 load -- so neither a release fence
+// per workgroup (a `buffer_wbl2` wrote back the default-policy output held in L2 and doubled the
+// C2 pass time) nor an acquire fence (~1.7 us) is needed. All threads must call it.
 template <int THREADS>
 __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t *done, uint32_t *s_ws,
                           uint32_t *s_flag) {
@@ -510,30 +511,34 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
     if (t == 0) *s_flag = atomicAdd(done, 1u) == gridDim.x - 1u ? 1u : 0u;
     __syncthreads();
     if (*s_flag == 0u) return;
-    // the acquire invalidates this CU's L1; no L2 holds a copy of the table (atomics drop the line,
-    // and nothing loaded it in this launch), so plain 16-B loads see every add
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // descriptor from uniform inputs only (kernel arguments): base and size readfirstlane'd
+    const uint64_t tb = (uint64_t)table;
+    const uint32_t lo32 = __builtin_amdgcn_readfirstlane((uint32_t)tb), hi32 = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
+    const uint32_t bytes = __builtin_amdgcn_readfirstlane((uint32_t)(m * 4));
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi32 << 32) | lo32), 0, bytes, 0x00020000);
+    auto ld = [&](uint32_t quad) {  // 16-B sc1 load (aux 16): L2-served, never a stale L1 line
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, quad * 16u, 0, 16));
+    };
     const uint64_t per = ((m + THREADS - 1) / THREADS + 3) & ~(uint64_t)3;
     const uint32_t beg = (uint32_t)(min(m, (uint64_t)t * per) / 4), end = (uint32_t)(min(m, (uint64_t)t * per + per) / 4);
-    u32x4 *q = reinterpret_cast<u32x4 *>(table);
-    // batches of 8 quads in flight (a latency-bound sweep: m = 20480 at C2 is 20 quads per thread)
-    constexpr uint32_t B = 8;
+    // batches of 12 quads in flight (a latency-bound sweep: m = 20480 at C2 is 20 quads per thread)
+    constexpr uint32_t B = 12;
     uint32_t s = 0;
     for (uint32_t i0 = beg; i0 < end; i0 += B) {
         u32x4 v[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? q[i0 + u] : u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? ld(i0 + u) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (uint32_t u = 0; u < B; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w;
     }
     uint32_t tot;
     uint32_t run = block_excl_scan<THREADS>(s, s_ws, tot);
+    u32x4 *q = reinterpret_cast<u32x4 *>(table);
     for (uint32_t i0 = beg; i0 < end; i0 += B) {
         u32x4 v[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? q[i0 + u] : u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? ld(i0 + u) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (uint32_t u = 0; u < B; ++u) {
             u32x4 o;
