@@ -55,7 +55,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--keys", "--n", dest="n", type=int, default=1 << 30, help="keys per GPU")
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--dist", choices=["uniform", "zipf", "equal"], default="uniform",
+                    help="key distribution (equal: every key the same, the clustered extreme)")
     ap.add_argument("--pairs", action="store_true")
     ap.add_argument("--rank", choices=["match", "split"], default="match")
     ap.add_argument("--tiles-per-chunk", type=int, default=0)
@@ -264,6 +265,8 @@ def main():
     keys = rs.empty_u32(n, dev)
     if a.dist == "uniform":
         rs.gen_uniform(keys, seed)
+    elif a.dist == "equal":
+        keys.fill_(0x1234567)
     else:
         sys.path.insert(0, str(ROOT / "tests"))
         from _util import zipf_cdf_u32
@@ -437,8 +440,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (splitmix64 uniform u32, seed 0x5EED, generated in HBM)"
-                    if a.dist == "uniform" else "synthetic (Zipf s=1.0 over 2^20 ranks, key=fmix32(rank))",
+            "data": {"uniform": "synthetic (splitmix64 uniform u32, seed 0x5EED, generated in HBM)",
+                     "zipf": "synthetic (Zipf s=1.0 over 2^20 ranks, key=fmix32(rank))",
+                     "equal": "synthetic (every key 0x01234567)"}[a.dist],
             "config": {"workload": f"sort {n} {'key+value pairs' if a.pairs else 'uint32 keys'} per GPU, "
                                    f"k={a.k} ({p.passes} passes), {a.dist}",
                        "keys_per_gpu": n, "k_bits": a.k, "passes": p.passes, "dist": a.dist,

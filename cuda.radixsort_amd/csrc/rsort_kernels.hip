@@ -286,15 +286,39 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
-    auto add = [&](uint32_t x) {
-        const uint32_t d = (x >> s0) & (R - 1u), e = (x >> s1) & (R - 1u);
+    // add inc (<= 64) to the 16-bit counter of pair (d, e); the add that takes it to 2^15 moves 2^15
+    // to the row's spill word and to the global count (the counter stays below 2^15 + 64)
+    auto add_pair = [&](uint32_t d, uint32_t e, uint32_t inc) {
         const uint32_t wi = d * RS + (e >> 1), sh = (e & 1u) << 4;
-        const uint32_t old = atomicAdd(&s_j[wi], 1u << sh);
-        if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+        const uint32_t before = (atomicAdd(&s_j[wi], inc << sh) >> sh) & 0xFFFFu;
+        if (before + inc >= 0x8000u && before < 0x8000u) {
             atomicSub(&s_j[wi], 0x8000u << sh);
             atomicAdd(&s_sp[d], 0x8000u);
             atomicAdd(&a.joint[e * R + d], 0x8000u);
         }
+    };
+    auto add = [&](uint32_t x) { add_pair((x >> s0) & (R - 1u), (x >> s1) & (R - 1u), 1u); };
+    // clustered input (runs of equal keys: sorted or duplicate-heavy data) sends a wave's lanes to
+    // one counter, where they serialise (all-equal keys: 64 lanes, ~128 cycles per instruction).
+    // Per 16-B quad: when most lanes hold 4 equal pairs, each such lane's 4 become one add of 4,
+    // and one lane adds for all lanes sharing the first lane's pair (as count_add); uniform keys
+    // pay one compare chain and one ballot per quad (the plain histogram's same4 test)
+    const uint32_t pmask = 0xFFFFu << s0;  // the pair's 16 bits (s0 <= 16 for a joint pass)
+    auto same4_of = [&](const u32x4 &q) { return (((q.x ^ q.y) | (q.x ^ q.z) | (q.x ^ q.w)) & pmask) == 0u; };
+    auto add4 = [&](const u32x4 &q) {
+        const uint32_t p0 = (q.x >> s0) & 0xFFu | ((q.x >> s1) & 0xFFu) << 8;
+        const bool same4 = same4_of(q);
+        if (!same4) {
+            add(q.x);
+            add(q.y);
+            add(q.z);
+            add(q.w);
+        }
+        // lanes with 4 equal pairs: the first such lane's pair once for all lanes sharing it
+        const uint32_t pa = __builtin_amdgcn_readfirstlane(same4 ? p0 : 0xFFFFFFFFu);
+        const uint64_t ma = __ballot(same4 && p0 == pa);
+        if (same4 && p0 != pa) add_pair(p0 & 0xFFu, p0 >> 8, 4u);
+        if (same4 && lane_id() == (uint32_t)__builtin_ctzll(ma)) add_pair(p0 & 0xFFu, p0 >> 8, 4u * (uint32_t)__popcll(ma));
     };
     const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
@@ -313,13 +337,21 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
                 const uint32_t v = v0 + u * THREADS;
                 q[u] = v < nvec ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
             }
+            // one clustering test per batch (the first quad): uniform keys take the plain adds
+            if (__popcll(__ballot(same4_of(q[0]))) < 32) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (v0 + u * THREADS < nvec) {
-                    add(q[u].x);
-                    add(q[u].y);
-                    add(q[u].z);
-                    add(q[u].w);
+                for (int u = 0; u < U; ++u) {
+                    if (v0 + u * THREADS < nvec) {
+                        add(q[u].x);
+                        add(q[u].y);
+                        add(q[u].z);
+                        add(q[u].w);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (v0 + u * THREADS < nvec) add4(q[u]);
                 }
             }
         }

@@ -102,6 +102,23 @@ def test_pass1_balanced_pass3_not():
     assert np.array_equal(y, oracle_sort(x, 8))
 
 
+@pytest.mark.parametrize("kind", ["equal", "runs"])
+def test_joint_count_clustered(kind):
+    """Pass 0's joint count on clustered input (rs_histogram JOINT, add4): all-equal keys (every
+    batch takes the aggregated adds; the 16-bit counters spill in steps of 4 x 64) and runs of 1..300
+    equal keys (batches of both kinds in one workgroup)."""
+    n = 768 * LINE_TILE - 7
+    rng = np.random.default_rng(23)
+    if kind == "equal":
+        x = np.full(n, 0x89ABCDEF, dtype=np.uint32)
+    else:
+        lens = rng.integers(1, 301, n // 100 + 2)
+        vals = rng.integers(0, 1 << 32, lens.size, dtype=np.uint64).astype(np.uint32)
+        x = np.repeat(vals, lens)[:n].copy()
+    y, _ = run(x, group_plan(n))
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
 @pytest.mark.parametrize("pairs", [False, True])
 def test_clustered_kernels(pairs):
     """Unbalanced groups select the clustered-input kernels (rank_add_hot) for passes 1..3. Input
