@@ -450,6 +450,10 @@ def main():
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
                        "group_chunk_passes": ([2 * i + 1 for i, f in enumerate(groups) if f]
                                               if groups is not None else None),
+                       # per odd pass: its digit groups, equal chunks cutting unbalanced groups, or
+                       # fixed chunks with a counted histogram (rsort_group_flags)
+                       "group_chunk_modes": ([("fixed", "groups", "cut")[f] for f in groups]
+                                             if groups is not None else None),
                        "parallelism": "single GPU" if not use_dist else
                        f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'})"},
             "verified": bool(verified),

@@ -168,6 +168,8 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     if (joint_plan(*p)) {
         ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
         ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
+        ws += align256((size_t)kPlanWords * 4);               // cut plan
+        ws += align256((size_t)kPieceSlots * kJointBins * 4); // its piece counts
     }
     if (!partition && next_plan(*p)) {
         ws += align256((size_t)p->table_entries * 4);  // the next pass's table
@@ -188,7 +190,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *table2, *done;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -211,6 +213,10 @@ Carve carve(const rsort_plan &p, void *ws) {
         q += align256((size_t)kJointBins * kJointBins * 4);
         c.bounds = (uint32_t *)q;
         q += align256((size_t)2 * kBoundsWords * 4);
+        c.plan = (uint32_t *)q;
+        q += align256((size_t)kPlanWords * 4);
+        c.pcounts = (uint32_t *)q;
+        q += align256((size_t)kPieceSlots * kJointBins * 4);
     }
     if (next_plan(p)) {
         c.table2 = (uint32_t *)q;
@@ -222,11 +228,11 @@ Carve carve(const rsort_plan &p, void *ws) {
 
 // ------------------------------------------------------------------------------ pass pieces
 // Joint pass (pass p of a joint_plan counting for pass p + 1): one workgroup per chunk counts
-// this pass's table and the joint counts; then the group bounds of pass p + 1. enable: nullptr,
-// or the previous joint pass's flag (its groups were unbalanced: count no joint either).
+// this pass's table and the joint counts; then the chunks of pass p + 1 (its digit groups, or
+// the cut plan). enable: nullptr, or the previous joint pass's flag (kGroupsFixed: no joint count).
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
-                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, hipStream_t s,
-                       bool zero_joint) {
+                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
+                       uint32_t *pcounts, hipStream_t s, bool zero_joint) {
     HistArgs a{};
     a.keys = keys;
     a.table = table;
@@ -244,17 +250,22 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess)
         return RSORT_ERR_HIP;
     if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
-    // a group may take one tile more than a fixed chunk
-    return hip_status(launch_joint_bounds(joint, enable, bounds, (uint64_t)p.n,
-                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, s));
+    // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
+    // group boundary up to half a tile (and a quarter chunk) away
+    const uint32_t snap = (uint32_t)std::min<int64_t>(p.tile_keys / 2, p.n / (4 * (int64_t)kJointBins));
+    return hip_status(launch_joint_bounds(joint, enable, bounds, plan, pcounts, (uint64_t)p.n,
+                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, s));
 }
 
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                  int dmode, const uint32_t *split, int nsplit, hipStream_t s,
-                 const uint32_t *bounds = nullptr, uint32_t *copy_src = nullptr) {
+                 const uint32_t *bounds = nullptr, uint32_t *copy_src = nullptr,
+                 const uint32_t *plan = nullptr, uint32_t *pcounts = nullptr) {
     HistArgs a{};
     a.bounds = bounds;
     a.copy_src = copy_src;
+    a.plan = plan;
+    a.pcounts = pcounts;
     a.keys = keys;
     a.table = table;
     a.n = (uint64_t)p.n;
@@ -270,9 +281,9 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
     const int64_t want = 4 * (int64_t)(cus > 0 ? cus : 256);  // 1024-thread workgroups (hist_bits)
     a.split = 1;
     if (bounds != nullptr) {
-        // a digit-group pass (256 chunks of one workgroup each): copies the joint counts, or counts
-        // one chunk per 1024-thread workgroup (as fast as split workgroups, 0.62 ms per 2^30 keys,
-        // and no table memset launch)
+        // a digit-group pass (256 chunks of one workgroup each): copies the joint counts, counts the
+        // cut plan's pieces, or counts one chunk per 1024-thread workgroup (as fast as split
+        // workgroups, 0.62 ms per 2^30 keys, and no table memset launch)
         a.wide = 1;
     } else if (p.num_chunks < want && p.chunk_keys >= 8 * 4096) {
         a.split = (uint32_t)std::min<int64_t>({(want + p.num_chunks - 1) / p.num_chunks, p.chunk_keys / 4096, 64});
@@ -283,9 +294,16 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
 }
 
 int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr,
-            uint32_t *done = nullptr) {
+            uint32_t *done = nullptr, const Carve *cut = nullptr, const uint32_t *group_flag = nullptr) {
     ScanArgs a{};
     a.done = done;
+    if (cut != nullptr) {
+        // a digit-group pass: under a cut plan the scan assembles the table first
+        a.group_flag = group_flag;
+        a.joint = cut->joint;
+        a.plan = cut->plan;
+        a.pcounts = cut->pcounts;
+    }
     a.table = table;
     a.block_sums = bsums;
     a.zero = zero;
@@ -392,15 +410,18 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
-                                         c.bounds + (i / 2) * kBoundsWords, s, i == 0)))
+                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0)))
                 return st;
         } else if (!(nextc && i > 0) &&
-                   (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint))) {
+                   (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
+                                      c.pcounts))) {
             return st;
         }
         // next-digit plans: pass 0's table is scanned by launches (which also arm the tail
         // counter); every later table was scanned by the previous scatter's last workgroup
-        if (!(nextc && i > 0) && (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr))) return st;
+        if (!(nextc && i > 0) &&
+            (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds)))
+            return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
         // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the
         // clustered-input kernel runs (rank_add_hot), else the plain one -- chosen on the device
@@ -642,8 +663,8 @@ int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flag
             hipMemcpyAsync(&h[i], c.bounds + i * kBoundsWords, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
             return RSORT_ERR_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
-    flags[0] = h[0] ? 1 : 0;
-    flags[1] = h[1] ? 1 : 0;
+    flags[0] = (int)h[0];  // kGroupsFixed / kGroupsWhole / kGroupsCut
+    flags[1] = (int)h[1];
     return RSORT_OK;
 }
 

@@ -70,10 +70,14 @@ struct HistArgs {
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
     // Digit-group chunks (kJointBits plans, see rs_histogram_joint). bounds != nullptr and
-    // bounds[0] != 0: this pass's table is copy_src (the previous pass's joint counts), copied
-    // instead of counted, and copy_src is cleared as it is read (the next counting pass adds into it).
+    // bounds[0] == kGroupsWhole: this pass's table is copy_src (the previous pass's joint counts),
+    // copied instead of counted, and copy_src is cleared as it is read (the next counting pass adds
+    // into it). bounds[0] == kGroupsCut: the workgroups count the cut plan's pieces (plan, below)
+    // into pcounts; the scan assembles the table.
     const uint32_t *bounds;
     uint32_t *copy_src;
+    const uint32_t *plan;
+    uint32_t *pcounts;
     uint32_t wide;          // 1: 1024-thread workgroups also with split == 1 (one per chunk, no memset)
     // rs_histogram_joint only: the joint counts [next digit][digit] are added into `joint`
     // (zeroed); joint_enable == nullptr or *joint_enable != 0 turns the joint count on.
@@ -94,7 +98,7 @@ struct ScatterArgs {
     uint32_t local_only;    // 1: write each tile's local order back in place of the tile
     uint32_t nsplit;
     uint32_t splitters[kMaxSplitters];
-    unsigned long long *stamps;  // diagnostic builds (RSORT_STAMPS) only: per-phase cycles
+    unsigned long long *stamps;  // unused by the library; dev/lines_exp.hip's per-phase cycle stamps
     // rs_scatter_lines only: bounds != nullptr and bounds[0] != 0 -> chunk c is the key range
     // [bounds[1 + c], bounds[2 + c]) (a digit group of the previous pass) instead of
     // [c * chunk_keys, (c + 1) * chunk_keys)
@@ -108,8 +112,8 @@ struct ScatterArgs {
     uint32_t *tail_zero;
     uint32_t *done;
     // k = 8 line kernels: != nullptr -> launch_scatter launches the plain and the clustered-input
-    // variant (rank_add_hot); *cl_select == 0 (a pass whose digit groups were unbalanced: skewed,
-    // duplicate-heavy keys) runs the clustered one, anything else the plain one
+    // variant (rank_add_hot); *cl_select == kGroupsWhole runs the plain one, anything else (a pass
+    // whose digit groups were unbalanced: skewed, duplicate-heavy keys) the clustered one
     const uint32_t *cl_select;
 };
 
@@ -121,6 +125,12 @@ struct ScanArgs {
     uint32_t *zero;         // optional: zero_n words cleared by the first launch
     uint64_t zero_n;
     uint32_t *done;         // optional: a tail-scan counter (ScatterArgs::done) zeroed by the first launch
+    // digit-group plans, odd passes: *group_flag == kGroupsCut -> the first launch assembles the
+    // table from the joint counts and the piece counts (cut_entry), the second clears `joint`
+    const uint32_t *group_flag;
+    uint32_t *joint;
+    const uint32_t *plan;
+    const uint32_t *pcounts;
 };
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.
@@ -131,13 +141,34 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
 // p + 1 reads no keys for its histogram.
 constexpr int kJointBits = 8;
 constexpr uint32_t kJointBins = 1u << kJointBits;
-constexpr uint32_t kBoundsWords = kJointBins + 2;  // {flag, group starts[0..R]}
+constexpr uint32_t kBoundsWords = kJointBins + 2;  // {flag, chunk starts[0..R]}
+// bounds[0]: how the next pass takes its chunks
+//   kGroupsFixed  fixed chunks, histogram counted from the keys (group path off)
+//   kGroupsWhole  the digit groups are the chunks (each fits max_keys): table = joint counts
+//   kGroupsCut    unbalanced groups (skewed keys): n / R-key chunks, each boundary snapped to a
+//                 group boundary within `snap` keys or cutting a group. A cut group's segments
+//                 but its largest are counted from the keys ("pieces"), the largest is its
+//                 joint column minus the others, every whole group in a chunk is its joint column.
+constexpr uint32_t kGroupsFixed = 0, kGroupsWhole = 1, kGroupsCut = 2;
+// Cut plan (workspace, rs_joint_bounds): header {pieces, counted keys}, per chunk c a descriptor
+// {first group gA | last group gB << 8 | head mode << 16 | tail mode << 18 | empty << 20} (head:
+// chunk c's part of gA, slot 2c; tail: its part of gB != gA, slot 2c + 1), per cut group
+// {first chunk | last chunk << 8 | derived slot << 16}, and the pieces {start, end, slot, offset
+// among the counted keys}. pcounts: kPieceSlots rows of R digit counts, one per slot.
+constexpr uint32_t kSegWhole = 0, kSegCounted = 1, kSegDerived = 2;
+constexpr uint32_t kPlanDesc = 16;
+constexpr uint32_t kPlanGroup = kPlanDesc + kJointBins;
+constexpr uint32_t kPlanPieces = kPlanGroup + kJointBins;
+constexpr uint32_t kPlanWords = kPlanPieces + 4 * kJointBins;
+constexpr uint32_t kPieceSlots = 2 * kJointBins;
 hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
-// From the joint counts [next digit][group]: group starts into bounds[1..R+1] and bounds[0] = 1
-// when every group fits in max_keys keys and the counts add up to n (else 0: the next pass
-// counts its own histogram over fixed chunks). enable: as HistArgs::joint_enable.
+// From the joint counts [next digit][group]: the next pass's chunks into bounds[1..R+1] and its
+// mode into bounds[0] (above): kGroupsWhole when every group fits in max_keys keys, else the cut
+// plan (plan, pcounts rows zeroed); kGroupsFixed when the counts do not add up to n or enable
+// says the joint count was off (HistArgs::joint_enable).
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
-                               uint64_t n, uint64_t max_keys, hipStream_t s);
+                               uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
+                               uint32_t snap, hipStream_t s);
 // rank_algo: internal RankAlgo. aligned16: kout/vout 16-B aligned (kGeomLines line stores;
 // otherwise the same plan runs rs_scatter with the same tiles).
 hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom, int aligned16,

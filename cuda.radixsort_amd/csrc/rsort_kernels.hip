@@ -271,7 +271,8 @@ struct Digit {
 // ordered by digit p, so pass p + 1 may take digit p's groups as its chunks: group g's counts of
 // digit p + 1 are the joint counts J[g][.] of (digit p, digit p + 1), which pass p counts here
 // (JOINT) while it reads the keys anyway. Pass p + 1's histogram launch then only copies them
-// (a.bounds[0] set by rs_joint_bounds when the groups are balanced enough to be chunks).
+// (a.bounds[0] == kGroupsWhole, set by rs_joint_bounds when the groups are balanced enough to be
+// chunks), or counts just the pieces of the groups its chunks cut (kGroupsCut).
 // Joint counts live in LDS as 2^16 16-bit counters, two per word, in rows of 128 + 1 words
 // (the pad makes the column sweep of the final add bank-conflict free); a counter that reaches
 // 2^15 moves 2^15 to its row's spill word and to the global count (the returning add tells).
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     const uint32_t S = a.split;
     const uint32_t c = blockIdx.x / S;
     const uint32_t sub = blockIdx.x % S;
-    if (a.bounds != nullptr && a.bounds[0] != 0u) {
+    if (a.bounds != nullptr && a.bounds[0] == kGroupsWhole) {
         // digit-group chunks: this pass's table is the previous pass's joint counts
         const uint64_t m = (uint64_t)R * a.num_chunks;
         for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < m; i += (uint64_t)gridDim.x * THREADS) {
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
         return;
     }
     if constexpr (JOINT) {
-        if (a.joint_enable == nullptr || *a.joint_enable != 0u) {
+        if (a.joint_enable == nullptr || *a.joint_enable == kGroupsWhole) {
             hist_joint_body<THREADS>(a, s_h, c, sub, S);
             return;
         }
@@ -413,56 +414,109 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     // counter of digit d: my[d * SB] (this lane's sub-counter)
     uint32_t *my = s_h + (HW > 1 ? (t / kWave) * R * SB : 0) + (SB > 1 ? lane_id() % SB : 0);
     const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
-    // this workgroup's part of chunk c: S parts of a multiple of 4 keys (16-B aligned starts)
-    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
-    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
-    const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
-    const uint64_t beg = min(cbeg + sub * part, cend);
-    const uint64_t end = min(beg + part, cend);
-    uint64_t tail = beg;
-    if (a.vec) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
-        const uint32_t nvec = (uint32_t)((end - beg) / 4);
-        constexpr int U = 4;
-        for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
-            u32x4 q[U];
+    // keys [beg, end) into the LDS counters (16-B loads from the first 16-B aligned key on)
+    auto count_range = [&](uint64_t beg, uint64_t end) {
+        uint64_t tail = beg;
+        if (a.vec) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const uint64_t vb = min((beg + 3) & ~(uint64_t)3, end);
+            for (uint64_t i = beg + t; i < vb; i += THREADS) atomicAdd(&my[dig(a.keys[i]) * SB], 1u);
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + vb);
+            const uint32_t nvec = (uint32_t)((end - vb) / 4);
+            constexpr int U = 4;
+            for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
+                u32x4 q[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t v = v0 + u * THREADS;
-                // NT: non-temporal loads (the keys are read once per pass)
-                q[u] = v < nvec ? (NT ? __builtin_nontemporal_load(p + v) : p[v]) : u32x4{0, 0, 0, 0};
-            }
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t v = v0 + u * THREADS;
+                    // NT: non-temporal loads (the keys are read once per pass)
+                    q[u] = v < nvec ? (NT ? __builtin_nontemporal_load(p + v) : p[v]) : u32x4{0, 0, 0, 0};
+                }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (v0 + u * THREADS < nvec) {
-                    const uint32_t dx = dig(q[u].x), dy = dig(q[u].y), dz = dig(q[u].z), dw = dig(q[u].w);
-                    const bool same4 = dx == dy && dy == dz && dz == dw;
-                    if (__popcll(__ballot(same4)) >= 32) {
-                        // clustered input (runs of equal keys, e.g. duplicates after a pass): one
-                        // add of 4 per lane, lanes sharing the common digits together
-                        if (same4) {
-                            // (count_add's aggregating lane adds for all: any sub-counter will do)
-                            if constexpr (SB > 1) count_add(my, dx * SB, 4u);
-                            else count_add(my, dx, 4u);
+                for (int u = 0; u < U; ++u) {
+                    if (v0 + u * THREADS < nvec) {
+                        const uint32_t dx = dig(q[u].x), dy = dig(q[u].y), dz = dig(q[u].z), dw = dig(q[u].w);
+                        const bool same4 = dx == dy && dy == dz && dz == dw;
+                        if (__popcll(__ballot(same4)) >= 32) {
+                            // clustered input (runs of equal keys, e.g. duplicates after a pass): one
+                            // add of 4 per lane, lanes sharing the common digits together
+                            if (same4) {
+                                // (count_add's aggregating lane adds for all: any sub-counter will do)
+                                if constexpr (SB > 1) count_add(my, dx * SB, 4u);
+                                else count_add(my, dx, 4u);
+                            } else {
+                                atomicAdd(&my[dx * SB], 1u);
+                                atomicAdd(&my[dy * SB], 1u);
+                                atomicAdd(&my[dz * SB], 1u);
+                                atomicAdd(&my[dw * SB], 1u);
+                            }
                         } else {
                             atomicAdd(&my[dx * SB], 1u);
                             atomicAdd(&my[dy * SB], 1u);
                             atomicAdd(&my[dz * SB], 1u);
                             atomicAdd(&my[dw * SB], 1u);
                         }
-                    } else {
-                        atomicAdd(&my[dx * SB], 1u);
-                        atomicAdd(&my[dy * SB], 1u);
-                        atomicAdd(&my[dz * SB], 1u);
-                        atomicAdd(&my[dw * SB], 1u);
                     }
                 }
             }
+            tail = vb + (uint64_t)nvec * 4;
         }
-        tail = beg + (uint64_t)nvec * 4;
+        for (uint64_t i = tail + t; i < end; i += THREADS) atomicAdd(&my[dig(a.keys[i]) * SB], 1u);
+    };
+    // this pass's counts of one digit (all copies), the counters cleared for the next range
+    auto take = [&](uint32_t d) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int w = 0; w < HW; ++w)
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                s += s_h[(w * R + d) * SB + u];
+                s_h[(w * R + d) * SB + u] = 0;
+            }
+        return s;
+    };
+    if constexpr (BITS == kJointBits && DMODE == kDigitShift) {
+        if (a.bounds != nullptr && a.bounds[0] == kGroupsCut) {
+            // cut plan (rs_joint_bounds): the workgroups split the counted pieces' keys evenly; each
+            // counts its share of every piece it meets, adds the counts into the piece's row and
+            // takes them from its group's derived row (zeroed; the scan adds the joint counts)
+            __shared__ uint32_t s_first;
+            const uint32_t np = a.plan[0], K = a.plan[1];
+            const uint64_t s0 = (uint64_t)K * blockIdx.x / gridDim.x, s1 = (uint64_t)K * (blockIdx.x + 1) / gridDim.x;
+            if (s0 >= s1) return;
+            if (t < np) {
+                const uint32_t off = a.plan[kPlanPieces + 4 * t + 3];
+                const uint32_t nxt = t + 1 < np ? a.plan[kPlanPieces + 4 * t + 7] : K;
+                if (off <= s0 && s0 < nxt) s_first = t;
+            }
+            __syncthreads();
+            for (uint32_t i = s_first; i < np; ++i) {
+                const uint32_t ps = a.plan[kPlanPieces + 4 * i], pe = a.plan[kPlanPieces + 4 * i + 1];
+                const uint32_t sl = a.plan[kPlanPieces + 4 * i + 2], off = a.plan[kPlanPieces + 4 * i + 3];
+                const uint32_t slot = sl & 0xFFFFu, dslot = sl >> 16;
+                if (off >= s1) break;
+                const uint64_t lo = max(s0, (uint64_t)off), hi = min(s1, (uint64_t)off + (pe - ps));
+                count_range(ps + (lo - off), ps + (hi - off));
+                __syncthreads();
+                for (uint32_t d = t; d < R; d += THREADS) {
+                    const uint32_t v = take(d);
+                    if (v) {
+                        atomicAdd(&a.pcounts[slot * R + d], v);
+                        atomicSub(&a.pcounts[dslot * R + d], v);  // the group's derived segment
+                    }
+                }
+                __syncthreads();
+            }
+            return;
+        }
     }
-    for (uint64_t i = tail + t; i < end; i += THREADS) atomicAdd(&my[dig(a.keys[i]) * SB], 1u);
+    // this workgroup's part of chunk c: S parts of a multiple of 4 keys (16-B aligned starts)
+    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
+    const uint64_t beg = min(cbeg + sub * part, cend);
+    const uint64_t end = min(beg + part, cend);
+    count_range(beg, end);
     __syncthreads();
     for (uint32_t d = t; d < R; d += THREADS) {
         uint32_t s = 0;
@@ -489,8 +543,63 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
     if (a.done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.done = 0u;
     const uint64_t base = (uint64_t)blockIdx.x * kScanSegment + (uint64_t)threadIdx.x * kScanPerThread;
     uint32_t s = 0;
+    if (a.group_flag != nullptr && *a.group_flag == kGroupsCut) {
+        // Cut plan (rs_joint_bounds): this block assembles digit rows d = 16 b .. 16 b + 15 of the
+        // R x R table [digit][chunk], thread c chunk c: its first group's part (the head, slot 2c),
+        // the whole groups after it (a difference of the row's prefix sums over the groups) and its
+        // last group's part (the tail, slot 2c + 1). A part that is a whole group is its joint
+        // count, a counted piece its row, the derived one (a cut group's largest part) the group's
+        // joint count plus its row (minus the group's counted pieces, rs_histogram).
+        static_assert(kScanThreads == (int)kJointBins && kScanSegment == kScanPerThread * (int)kJointBins,
+                      "one scan block = 16 rows of 256 chunks");
+        constexpr uint32_t R = kJointBins, NW = kScanThreads / kWave, RP = R + 1;
+        __shared__ uint32_t s_pj[kScanPerThread * RP];   // per row: prefix over groups, [0] = 0
+        __shared__ uint32_t s_wt[kScanPerThread * NW];   // per row and wave: the wave's total
+        const uint32_t c = threadIdx.x, w = c / kWave, d0 = blockIdx.x * kScanPerThread;
+        const uint32_t dc = a.plan[kPlanDesc + c];
+        const uint32_t gA = dc & 255u, gB = (dc >> 8) & 255u, hm = (dc >> 16) & 3u, tm = (dc >> 18) & 3u;
+        const bool empty = (dc >> 20) != 0u;
+        uint32_t jv[kScanPerThread], hv[kScanPerThread], tv[kScanPerThread];
 #pragma unroll
-    for (int i = 0; i < kScanPerThread; ++i) s += (base + i < a.m) ? a.table[base + i] : 0u;
+        for (int i = 0; i < kScanPerThread; ++i) {
+            jv[i] = a.joint[(d0 + i) * R + c];  // group c's count of digit d0 + i
+            hv[i] = hm != kSegWhole ? a.pcounts[(2u * c) * R + d0 + i] : 0u;
+            tv[i] = tm != kSegWhole ? a.pcounts[(2u * c + 1u) * R + d0 + i] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kScanPerThread; ++i) {
+            jv[i] = wave_incl_scan(jv[i]);
+            if (lane_id() == kWave - 1) s_wt[i * NW + w] = jv[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kScanPerThread; ++i) {
+            uint32_t add = 0;
+#pragma unroll
+            for (uint32_t x = 0; x < NW; ++x) add += x < w ? s_wt[i * NW + x] : 0u;
+            s_pj[i * RP + c + 1] = jv[i] + add;
+        }
+        if (c < kScanPerThread) s_pj[c * RP] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kScanPerThread; ++i) {
+            const uint32_t *pj = s_pj + i * RP;
+            uint32_t v = 0;
+            if (!empty) {
+                const uint32_t ja = pj[gA + 1] - pj[gA];
+                v = hm == kSegWhole ? ja : hv[i] + (hm == kSegDerived ? ja : 0u);
+                if (gB != gA) {
+                    const uint32_t jb = pj[gB + 1] - pj[gB];
+                    v += (pj[gB] - pj[gA + 1]) + (tm == kSegWhole ? jb : tv[i] + (tm == kSegDerived ? jb : 0u));
+                }
+            }
+            a.table[(d0 + i) * R + c] = v;
+            s += v;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanPerThread; ++i) s += (base + i < a.m) ? a.table[base + i] : 0u;
+    }
     uint32_t tot;
     block_excl_scan<kScanThreads>(s, s_ws, tot);
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
@@ -505,6 +614,12 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
     block_excl_scan<kScanThreads>(pre, s_ws, prefix);
 
     const uint64_t base = (uint64_t)b * kScanSegment + (uint64_t)threadIdx.x * kScanPerThread;
+    if (a.group_flag != nullptr && *a.group_flag == kGroupsCut) {
+        // the joint counts were read by the first launch: clear them for the next joint count
+        // (the table is R x R, the joint counts' shape)
+        for (int i = 0; i < kScanPerThread; ++i)
+            if (base + i < a.m) a.joint[base + i] = 0u;
+    }
     uint32_t v[kScanPerThread];
     uint32_t s = 0;
 #pragma unroll
@@ -589,18 +704,25 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
 
 // ------------------------------------------------------------------------------ group bounds
 // One workgroup: group totals (column sums of the joint counts [next digit][group]), their
-// exclusive scan = the groups' first key positions in the previous pass's output, and the flag
-// that lets the next pass use them as chunks.
+// exclusive scan = the groups' first key positions in the previous pass's output, and the next
+// pass's chunk mode (kGroupsWhole / kGroupsCut / kGroupsFixed, rsort_internal.hpp) with its
+// chunk starts; for kGroupsCut also the cut plan and zeroed piece rows.
 __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, const uint32_t *enable,
-                                                        uint32_t *bounds, uint64_t n, uint64_t max_keys) {
+                                                        uint32_t *bounds, uint32_t *plan, uint32_t *pcounts,
+                                                        uint64_t n, uint64_t max_keys, uint32_t snap) {
     constexpr uint32_t R = kJointBins;
     constexpr uint32_t Q = 1024 / R;
     __shared__ uint32_t s_part[Q][R];
     __shared__ uint32_t s_ws[1024 / kWave];
     __shared__ uint32_t s_max;
+    __shared__ uint32_t s_b[R + 1];                // group starts
+    __shared__ uint32_t s_B[R + 1];                // chunk starts (cut plan)
+    __shared__ unsigned long long s_big[R];        // cut group: largest segment (size << 10 | slot)
+    __shared__ uint32_t s_cf[R], s_cl[R];          // cut group: first and last chunk
+    __shared__ uint32_t s_slot[R];                 // counted pieces' slots
     const uint32_t t = threadIdx.x;
-    if (enable != nullptr && *enable == 0u) {
-        if (t == 0) bounds[0] = 0u;
+    if (enable != nullptr && *enable != kGroupsWhole) {  // no joint count this pass
+        if (t == 0) bounds[0] = kGroupsFixed;
         return;
     }
     const uint32_t g = t % R, q = t / R;
@@ -617,10 +739,126 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     }
     uint32_t total = 0;
     const uint32_t start = block_excl_scan<1024>(tot, s_ws, total);
-    if (t < R) bounds[1 + t] = start;
+    if ((uint64_t)total != n) {
+        if (t == 0) bounds[0] = kGroupsFixed;
+        return;
+    }
+    if ((uint64_t)s_max <= max_keys) {
+        if (t < R) bounds[1 + t] = start;
+        if (t == 0) {
+            bounds[1 + R] = total;
+            bounds[0] = kGroupsWhole;
+        }
+        return;
+    }
+    // ---- cut plan: chunk c starts near c * n / R
+    if (plan == nullptr) {  // (callers without a plan area: fixed chunks)
+        if (t == 0) bounds[0] = kGroupsFixed;
+        return;
+    }
+    if (t < R) {
+        s_b[t] = start;
+        s_big[t] = 0ull;
+        s_cf[t] = 0xFFFFFFFFu;
+        s_cl[t] = 0u;
+    }
+    if (t == 0) s_b[R] = total;
+    __syncthreads();
+    // the group holding position x < n: the last g with s_b[g] <= x (its end is past x)
+    auto group_of = [&](uint32_t x) {
+        uint32_t lo = 0, hi = R - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (s_b[mid] <= x) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    if (t <= R) {
+        uint32_t B = (uint32_t)((n * t) / R);
+        if (t > 0 && t < R) {
+            // snap to the nearer group boundary when it is within `snap` keys
+            const uint32_t gg = group_of(B);
+            const uint32_t d0 = B - s_b[gg], d1 = s_b[gg + 1] - B;
+            if (min(d0, d1) <= snap) B = d0 <= d1 ? s_b[gg] : s_b[gg + 1];
+        }
+        s_B[t] = B;
+        bounds[1 + t] = B;
+    }
+    __syncthreads();
+    // per chunk: its first and last group and their segments in it
+    uint32_t gA = 0, gB = 0, hb = 0, he = 0, tb = 0, te = 0;
+    bool empty = true, hpart = false, tpart = false;
+    if (t < R) {
+        const uint32_t b = s_B[t], e = s_B[t + 1];
+        empty = b >= e;
+        if (!empty) {
+            gA = group_of(b);
+            gB = group_of(e - 1);
+            hb = b;
+            he = min(e, s_b[gA + 1]);
+            hpart = hb > s_b[gA] || he < s_b[gA + 1];
+            if (gB != gA) {
+                tb = s_b[gB];
+                te = e;
+                tpart = te < s_b[gB + 1];
+            }
+            if (hpart) {
+                atomicMax(&s_big[gA], ((unsigned long long)(he - hb) << 10) | (2u * t));
+                atomicMin(&s_cf[gA], t);
+                atomicMax(&s_cl[gA], t);
+            }
+            if (tpart) {
+                atomicMax(&s_big[gB], ((unsigned long long)(te - tb) << 10) | (2u * t + 1u));
+                atomicMin(&s_cf[gB], t);
+                atomicMax(&s_cl[gB], t);
+            }
+        }
+    }
+    __syncthreads();
+    // each cut group's largest segment is derived, the others are counted
+    uint32_t hm = kSegWhole, tm = kSegWhole;
+    if (hpart) hm = (uint32_t)(s_big[gA] & 1023u) == 2u * t ? kSegDerived : kSegCounted;
+    if (tpart) tm = (uint32_t)(s_big[gB] & 1023u) == 2u * t + 1u ? kSegDerived : kSegCounted;
+    const uint32_t npc = (hm == kSegCounted ? 1u : 0u) + (tm == kSegCounted ? 1u : 0u);
+    const uint32_t nkc = (hm == kSegCounted ? he - hb : 0u) + (tm == kSegCounted ? te - tb : 0u);
+    uint32_t np = 0, K = 0;
+    uint32_t pi = block_excl_scan<1024>(npc, s_ws, np);
+    uint32_t ko = block_excl_scan<1024>(nkc, s_ws, K);
+    if (t < R) {
+        plan[kPlanDesc + t] = gA | (gB << 8) | (hm << 16) | (tm << 18) | ((empty ? 1u : 0u) << 20);
+        plan[kPlanGroup + t] = (s_cf[t] & 255u) | ((s_cl[t] & 255u) << 8) | ((uint32_t)(s_big[t] & 1023u) << 16);
+        if (hm == kSegCounted) {
+            uint32_t *pc = plan + kPlanPieces + 4 * pi;
+            pc[0] = hb;
+            pc[1] = he;
+            pc[2] = (2u * t) | ((uint32_t)(s_big[gA] & 1023u) << 16);
+            pc[3] = ko;
+            s_slot[pi] = 2u * t;
+            ++pi;
+            ko += he - hb;
+        }
+        if (tm == kSegCounted) {
+            uint32_t *pc = plan + kPlanPieces + 4 * pi;
+            pc[0] = tb;
+            pc[1] = te;
+            pc[2] = (2u * t + 1u) | ((uint32_t)(s_big[gB] & 1023u) << 16);
+            pc[3] = ko;
+            s_slot[pi] = 2u * t + 1u;
+        }
+    }
     if (t == 0) {
-        bounds[1 + R] = total;
-        bounds[0] = ((uint64_t)total == n && (uint64_t)s_max <= max_keys) ? 1u : 0u;
+        plan[0] = np;
+        plan[1] = K;
+        bounds[0] = kGroupsCut;
+    }
+    __syncthreads();
+    // the counted pieces' rows and each cut group's derived row start at zero (the histogram
+    // launch adds every piece's counts into its row and takes them from its group's derived row)
+    for (uint32_t i = t; i < np * R; i += 1024) pcounts[s_slot[i / R] * R + i % R] = 0u;
+    for (uint32_t i = t; i < R * R; i += 1024) {
+        const uint32_t gg = i / R, d = i % R;
+        if (s_big[gg] != 0ull) pcounts[(uint32_t)(s_big[gg] & 1023u) * R + d] = 0u;
     }
 }
 
@@ -970,7 +1208,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     uint32_t head = 0;  // leading keys of the first tile that belong to the previous chunk
     // clustered-pass selection (ScatterArgs::cl_select): the plain and the clustered kernel are both
     // launched, and the one not selected by the device-side flag leaves at once
-    if (a.cl_select != nullptr && ((*a.cl_select == 0u) != (CL != 0))) return;
+    if (a.cl_select != nullptr && ((*a.cl_select != kGroupsWhole) != (CL != 0))) return;
     if (a.bounds != nullptr && a.bounds[0] != 0u) {
         // digit-group chunk (rs_histogram_joint): any start, so the tiles start at the 256-B
         // boundary below it (every wave load stays two whole 128-B lines), the first tile skips
@@ -1739,8 +1977,9 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
-                               uint64_t n, uint64_t max_keys, hipStream_t s) {
-    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, n, max_keys);
+                               uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
+                               uint32_t snap, hipStream_t s) {
+    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap);
     return hipGetLastError();
 }
 

@@ -325,8 +325,9 @@ def sort_device(keys_in, keys_out, k_bits=8, vals_in=None, vals_out=None, ws=Non
 
 
 def group_flags(p: Plan, ws, stream=None) -> list[int]:
-    """Which odd passes (1, 3) of the last sort with plan `p` and workspace `ws` ran on digit-group
-    chunks (rsort_group_flags; synchronises the stream)."""
+    """How the odd passes (1, 3) of the last sort with plan `p` and workspace `ws` took their chunks
+    (rsort_group_flags; synchronises the stream): 1 digit groups, 2 equal chunks cutting unbalanced
+    groups, 0 fixed chunks with counted histograms."""
     flags = (ctypes.c_int * 2)()
     _check(_lib().rsort_group_flags(ctypes.byref(p), _ptr(ws), flags, _stream(stream)), "rsort_group_flags")
     return [int(flags[0]), int(flags[1])]

@@ -47,6 +47,36 @@ __global__ __launch_bounds__(THREADS) void runs(const u32x4 *__restrict__ in, ui
     }
 }
 
+// the same for key + value pairs: two input arrays read, two output arrays written with the same
+// runs (a pairs pass: 8192-pair tiles, 256 regions -> runs of 32 pairs = 128 B per array)
+template <int THREADS, int QPT>
+__global__ __launch_bounds__(THREADS) void runs_pairs(const u32x4 *__restrict__ in, const u32x4 *__restrict__ vin,
+                                                       uint32_t *__restrict__ out, uint32_t *__restrict__ vout,
+                                                       uint64_t n, uint32_t L, uint32_t tpc, uint32_t skew) {
+    constexpr uint32_t T = THREADS * QPT * 4;
+    const uint32_t R = T / L;
+    const uint64_t region = n / R - 32;
+    const uint64_t cbeg = (uint64_t)blockIdx.x * tpc * T;
+    for (uint32_t tile = 0; tile < tpc; ++tile) {
+        const uint64_t tb = cbeg + (uint64_t)tile * T;
+        if (tb + T > n) break;
+        u32x4 v[QPT], w[QPT];
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            v[j] = in[tb / 4 + threadIdx.x + j * THREADS];
+            w[j] = vin[tb / 4 + threadIdx.x + j * THREADS];
+        }
+#pragma unroll
+        for (int j = 0; j < QPT; ++j) {
+            const uint32_t i = (threadIdx.x + j * THREADS) * 4;
+            const uint32_t r = i / L;
+            const uint64_t pos = r * region + skew + (uint64_t)blockIdx.x * tpc * L + (uint64_t)tile * L + (i % L);
+            __builtin_nontemporal_store(v[j], reinterpret_cast<u32x4 *>(out + pos));
+            __builtin_nontemporal_store(w[j], reinterpret_cast<u32x4 *>(vout + pos));
+        }
+    }
+}
+
 template <int THREADS, int QPT>
 __global__ __launch_bounds__(THREADS) void copy(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, uint64_t n4) {
     for (uint64_t b = (uint64_t)blockIdx.x * THREADS * QPT; b < n4; b += (uint64_t)gridDim.x * THREADS * QPT) {
@@ -104,6 +134,32 @@ int main(int argc, char **argv) {
         snprintf(nm, sizeof nm, "256 regions, %5u-key tiles: runs of %u keys", T, T / 256);
         timeit(nm, [&] { runs<TH, Q><<<g, TH>>>((const u32x4 *)a, b, n, T / 256, tpc, 0); });
     };
+    {
+        // pairs: 2^lg pairs = two arrays each way (16 B per pair); value buffers of the same size
+        uint32_t *va, *vb;
+        CK(hipMalloc(&va, n * 4));
+        CK(hipMalloc(&vb, n * 4));
+        CK(hipMemset(va, 3, n * 4));
+        for (uint32_t skew : {0u, 16u}) {
+            constexpr int TH = 512, Q = 4;  // 8192-pair tiles
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            snprintf(nm, sizeof nm, "pairs, 8192-pair tiles, runs of 32, skew %u (x2 bytes)", skew);
+            timeit(nm, [&] { runs_pairs<TH, Q><<<g, TH>>>((const u32x4 *)a, (const u32x4 *)va, b, vb, n, T / 256, tpc, skew); });
+        }
+        {
+            constexpr int TH = 1024, Q = 4;  // 16384-pair tiles: runs of 64 pairs
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            timeit("pairs, 16384-pair tiles, runs of 64 (x2 bytes)", [&] { runs_pairs<TH, Q><<<g, TH>>>((const u32x4 *)a, (const u32x4 *)va, b, vb, n, T / 256, tpc, 0); });
+        }
+        CK(hipFree(va));
+        CK(hipFree(vb));
+    }
     regions256(std::integral_constant<int, 4>{});
     regions256(std::integral_constant<int, 6>{});
     regions256(std::integral_constant<int, 8>{});

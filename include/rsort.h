@@ -169,15 +169,18 @@ RSORT_API int rsort_get_rank_algo(void);
 /* Histograms carried between passes (default on), so passes read no keys for their histogram:
  *  - k = 8 plans with 256 chunks (digit-group chunks): every second pass takes the previous
  *    pass's digit groups as its chunks (the pass before counts (digit, next digit) pairs while
- *    it reads the keys);
+ *    it reads the keys); where the groups are unbalanced (skewed keys) it takes equal chunks
+ *    and reads only the keys of the groups those chunks cut (all but each cut group's largest
+ *    segment);
  *  - k = 3, 4 keys-only plans (next-digit counts): every pass adds the next pass's chunk table
  *    from where it writes each key; only pass 0 reads keys for a histogram.
  * Off: every pass counts its own histogram. Same output either way; process-wide. */
 RSORT_API int rsort_set_group_chunks(int enable);
 RSORT_API int rsort_get_group_chunks(void);
-/* After a sort with `plan` and `d_workspace` has completed on `stream`: flags[i] = 1 if odd pass
- * 2i+1 ran on digit-group chunks, else 0 (i < 2; both 0 for plans without group chunks).
- * Synchronises the stream. */
+/* After a sort with `plan` and `d_workspace` has completed on `stream`: flags[i] says how odd
+ * pass 2i+1 took its chunks (i < 2): 1 = the digit groups, 2 = equal chunks cutting unbalanced
+ * groups (counted pieces), 0 = fixed chunks with a counted histogram (group chunks off, or plans
+ * without them). Synchronises the stream. */
 RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
                                 void *stream);
 /* 1 if the current device's LDS returns same-address atomic adds in lane order (the default

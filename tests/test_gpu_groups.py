@@ -1,8 +1,9 @@
 """GPU parity of digit-group chunks (k = 8 plans with 256 chunks; rs_histogram_joint and
 rsort_capi.cpp sort_planned): passes 1 and 3 take the previous pass's digit groups as chunks and
 copy their histogram from the joint (digit, next digit) counts the pass before counted.
+Where the groups are unbalanced, passes 1 and 3 take equal chunks cutting them (cut plans).
 Bit-exact against the oracle (Baseline1.cu:15-64 restated) with the path on and off, and the
-flags say which passes actually ran on groups. Runs on the MI355X box (-m gpu)."""
+flags say how each odd pass took its chunks. Runs on the MI355X box (-m gpu)."""
 import numpy as np
 import pytest
 
@@ -56,13 +57,71 @@ def test_uniform_keys_on_groups(n):
     assert np.array_equal(y0, want)
 
 
-def test_zipf_keys_fall_back():
-    """Zipf digit groups are far from balanced: passes 1 and 3 count their own histograms."""
+def test_zipf_keys_cut_plan():
+    """Zipf digit groups are far from balanced: pass 1 takes equal chunks that cut the big groups
+    (kGroupsCut) and counts only the cut groups' pieces; pass 2 then counts no joint counts (on
+    clustered input they cost more than pass 3's count), so pass 3 counts its own."""
     n = 768 * LINE_TILE - 3
     x = zipf_keys(n, seed=7)
     y, flags = run(x, group_plan(n))
-    assert flags == [0, 0]
+    assert flags == [2, 0]
     assert np.array_equal(y, oracle_sort(x, 8))
+    y0, flags0 = run(x, group_plan(n), groups=False)
+    assert flags0 == [0, 0]
+    assert np.array_equal(y0, y)
+
+
+def _cut_input(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    x = uniform_keys(n, seed=seed)
+    if kind == "one_group":
+        # every key has digits 0 and 2 = 0x5A: passes 1 and 3 see one group of n keys (255 pieces)
+        return ((x & np.uint32(0xFF00FF00)) | np.uint32(0x005A005A)).astype(np.uint32)
+    if kind == "half_hot":
+        # half the keys have digit 0 = 7 (a group of ~128 chunks), the rest spread: small groups
+        # of half a chunk, boundaries cutting them
+        m = rng.random(n) < 0.5
+        x[m] = (x[m] & np.uint32(0xFFFFFF00)) | np.uint32(7)
+        return x
+    if kind == "two_chunk_groups":
+        # digit 0 in 0..127 only, equally often: groups of ~2 chunks, every second boundary inside
+        # one (two equal segments: the tie picks the derived one by slot)
+        d0 = (np.arange(n, dtype=np.uint64) * 128 // n).astype(np.uint32)
+        rng.shuffle(d0)
+        return ((x & np.uint32(0xFFFFFF00)) | d0).astype(np.uint32)
+    assert kind == "steps"
+    # group sizes 1, 2, 4, ... keys up to whole chunks and past them, plus empty groups
+    sizes = np.zeros(256, np.int64)
+    sizes[::3] = np.minimum(2 ** (np.arange(0, 256, 3) % 24), n)
+    sizes = (sizes * (n / sizes.sum())).astype(np.int64)
+    sizes[0] += n - sizes.sum()
+    d0 = np.repeat(np.arange(256, dtype=np.uint32), sizes)
+    rng.shuffle(d0)
+    return ((x & np.uint32(0xFFFFFF00)) | d0).astype(np.uint32)
+
+
+@pytest.mark.parametrize("kind", ["one_group", "half_hot", "two_chunk_groups", "steps"])
+@pytest.mark.parametrize("n", [512 * LINE_TILE, 768 * LINE_TILE - 13])
+def test_cut_plan_shapes(kind, n):
+    """Cut plans (rs_joint_bounds kGroupsCut, pieces counted by rs_histogram, table assembled by
+    rs_scan_reduce's cut_entry) on group shapes that hit every case: chunks inside one group,
+    chunks spanning many small groups, boundaries snapped onto group boundaries, equal segments,
+    empty groups. Bit-exact against the oracle."""
+    x = _cut_input(kind, n, seed=n % 1000 + len(kind))
+    y, flags = run(x, group_plan(n))
+    assert flags[0] == 2
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
+@pytest.mark.parametrize("kind", ["half_hot", "one_group"])
+def test_cut_plan_pairs(kind):
+    n = 768 * PAIRS_TILE - 5
+    x = _cut_input(kind, n, seed=41)
+    v = np.arange(n, dtype=np.uint32)
+    (ko, vo), flags = run(x, group_plan(n, pairs=True), vals=v)
+    assert flags[0] == 2
+    wk, wv = oracle_sort_pairs(x, v, 8)
+    assert np.array_equal(ko, wk) and np.array_equal(vo, wv)
 
 
 def test_joint_counter_spill():
@@ -94,11 +153,11 @@ def test_empty_groups():
 
 
 def test_pass1_balanced_pass3_not():
-    """Uniform low 16 bits, constant digit 2: pass 1 runs on groups, pass 3 falls back."""
+    """Uniform low 16 bits, constant digit 2: pass 1 runs on groups, pass 3 cuts the one group."""
     n = 768 * LINE_TILE - 1
     x = (uniform_keys(n, seed=9) & np.uint32(0xFF00FFFF)) | np.uint32(0x00AB0000)
     y, flags = run(x, group_plan(n))
-    assert flags == [1, 0]
+    assert flags == [1, 2]
     assert np.array_equal(y, oracle_sort(x, 8))
 
 
@@ -140,7 +199,7 @@ def test_clustered_kernels(pairs):
     x[rng.random(n) < 0.1] = hot[0]
     v = np.arange(n, dtype=np.uint32) if pairs else None
     out, flags = run(x, group_plan(n, pairs=pairs), vals=v)
-    assert flags == [0, 0]
+    assert flags == [2, 0]
     if pairs:
         wk, wv = oracle_sort_pairs(x, v, 8)
         assert np.array_equal(out[0], wk) and np.array_equal(out[1], wv)
@@ -154,7 +213,7 @@ def test_pairs_on_groups(dist):
     x = uniform_keys(n, seed=3) if dist == "uniform" else zipf_keys(n, seed=3)
     v = np.arange(n, dtype=np.uint32)
     (ko, vo), flags = run(x, group_plan(n, pairs=True), vals=v)
-    assert flags == ([1, 1] if dist == "uniform" else [0, 0])
+    assert flags == ([1, 1] if dist == "uniform" else [2, 0])
     wk, wv = oracle_sort_pairs(x, v, 8)
     assert np.array_equal(ko, wk) and np.array_equal(vo, wv)
 
