@@ -57,7 +57,31 @@ using namespace rsort;
 #endif
 
 enum { kOutB = 1, kRank1 = 2, kOutB2 = 4, kSB16 = 8, kPrio = 16, kCopy64 = 32, kSB4 = 64, kHot2 = 128, kRuns = 256,
-       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384, kCopyR = 32768, kStSc1 = 65536, kStPlain = 131072, kStNtSc1 = 262144 };
+       kRunsAgg = 512, kGate = 1024, kGate128 = 2048, kGateW = 4096, kPad = 8192, kCopyI = 16384, kCopyR = 32768, kStSc1 = 65536, kStPlain = 131072, kStNtSc1 = 262144,
+       kPeer = 524288, kPeerHot = 1048576 };
+
+// kPeer: every lane finds the lanes sharing its digit (BITS ballots), the lowest of them adds the
+// group's count with one returning add (no two lanes of an instruction on one counter), the
+// others read the base from it (ds_bpermute) and add their rank in the group (mbcnt).
+// kPeerHot: rank_add_hot's first-lane aggregation when >= 16 lanes share it, else kPeer.
+template <int BITS>
+__device__ __forceinline__ uint32_t rank_peer(uint32_t *cnt, uint32_t d) {
+    uint32_t mlo, mhi;
+    peer_mask<BITS>(d, mlo, mhi);
+    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t o = 0;
+    if (lane_id() == leader) o = atomicAdd(&cnt[d], (uint32_t)__popcll(m));
+    const uint32_t base = (uint32_t)__shfl((int)o, (int)leader);
+    return base + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+}
+template <int BITS>
+__device__ __forceinline__ uint32_t rank_peer_hot(uint32_t *cnt, uint32_t d) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t ma = __ballot(d == da);
+    if (__popcll(ma) >= 16) return agg_add(cnt, d, da, ma);
+    return rank_peer<BITS>(cnt, d);
+}
 
 // agg_add and rank_add_hot (kHot2) are the library's (rsort_kernels.hip)
 
@@ -241,7 +265,9 @@ __global__ __launch_bounds__(THREADS) void lx_lines(ScatterArgs a) {
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
                     uint32_t r;
-                    if constexpr ((V & kHot2) != 0) r = rank_add_hot(&s_cnt[w * RS], dj, hotd);
+                    if constexpr ((V & kPeer) != 0) r = rank_peer<BITS>(&s_cnt[w * RS], dj);
+                    else if constexpr ((V & kPeerHot) != 0) r = rank_peer_hot<BITS>(&s_cnt[w * RS], dj);
+                    else if constexpr ((V & kHot2) != 0) r = rank_add_hot(&s_cnt[w * RS], dj, hotd);
                     else if constexpr ((V & kRuns) != 0) r = rank_runs<false>(&s_cnt[w * RS], dj);
                     else if constexpr ((V & kRunsAgg) != 0) r = rank_runs<true>(&s_cnt[w * RS], dj);
                     else r = rank_add(&s_cnt[w * RS], dj);
@@ -677,6 +703,10 @@ int main(int argc, char **argv) {
         run<8, 1024, 16>(c, "lx pad sc1", lx_lines<8, 1024, 16, 32, OC | kPad | kStSc1>, g_shift);
         run<8, 1024, 16>(c, "lx pad nt sc1", lx_lines<8, 1024, 16, 32, OC | kPad | kStNtSc1>, g_shift);
         run<8, 1024, 16>(c, "lx pad plain", lx_lines<8, 1024, 16, 32, OC | kPad | kStPlain>, g_shift);
+        run<8, 1024, 16>(c, "lib CL rs_scatter_lines<...,3,1>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3, 1>, g_shift);
+        run<8, 1024, 16>(c, "lx pad hot2", lx_lines<8, 1024, 16, 32, OC | kPad | kHot2>, g_shift);
+        run<8, 1024, 16>(c, "lx pad peer", lx_lines<8, 1024, 16, 32, OC | kPad | kPeer>, g_shift);
+        run<8, 1024, 16>(c, "lx pad peerhot", lx_lines<8, 1024, 16, 32, OC | kPad | kPeerHot>, g_shift);
     }
     return 0;
 }

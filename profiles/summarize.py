@@ -51,10 +51,11 @@ def main(src: str, tag: str, n: int = 1 << 30, k: int = 8, dist: str = "uniform"
         vals = [v for (kn, c), vs in agg.items() if c == counter and needle in kn for v in vs]
         return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
-    # calibrate on the key-reading histogram launches only (digit-group passes' rs_histogram
-    # launches copy a 256-KiB table instead): those above a quarter of the expected 4n/2 bytes
+    # calibrate on the histogram launches that read all n keys only (digit-group passes'
+    # rs_histogram launches copy a 256-KiB table instead, cut-plan passes count a part of the
+    # keys): those within 20% of the expected 4n/2 bytes
     hvals = [v for (kn, c), vs in fetch.items() if c == "FETCH_SIZE" and "rs_histogram" in kn
-             for v in vs if v * 1024.0 > 0.25 * 2.0 * n]
+             for v in vs if 0.8 * 2.0 * n < v * 1024.0 < 1.25 * 2.0 * n]
     hist_fetch = sum(hvals) / len(hvals) if hvals else None
     gen_write, _ = per_launch(write, "WRITE_SIZE", "rs_gen_uniform" if dist == "uniform" else "rs_gen_zipf")
     # scatter launches that did the pass: the k = 8 kernels come as a plain and a clustered-input
