@@ -113,6 +113,23 @@ def test_cut_plan_shapes(kind, n):
     assert np.array_equal(y, oracle_sort(x, 8))
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_cut_plan_random_shapes(seed):
+    """Random group shapes for pass 1 (digit 0) and pass 3 (digit 2): Dirichlet group sizes with
+    a few heavy groups, empty groups, ragged n. Bit-exact against the oracle."""
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.choice([768, 1024])) * LINE_TILE - int(rng.integers(0, 4096))
+    x = uniform_keys(n, seed=200 + seed)
+    for shift in (0, 16):
+        w = rng.dirichlet(np.full(256, rng.choice([0.05, 0.3, 1.0])))
+        w[rng.integers(0, 256, int(rng.integers(0, 4)))] += rng.uniform(0.01, 0.3)
+        d = rng.choice(256, size=n, p=w / w.sum()).astype(np.uint32)
+        x = ((x & ~np.uint32(0xFF << shift)) | (d << np.uint32(shift))).astype(np.uint32)
+    y, flags = run(x, group_plan(n))
+    assert flags[0] in (1, 2)
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
 @pytest.mark.parametrize("kind", ["half_hot", "one_group"])
 def test_cut_plan_pairs(kind):
     n = 768 * PAIRS_TILE - 5
