@@ -638,8 +638,8 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 
 // The same exclusive scan as the tail of a kernel whose workgroups ADD into `table` with agent-scope
 // atomics (m entries, a multiple of 4, 16-B aligned, < 4 GiB): every workgroup waits for its adds and
-// bumps *done; the one whose bump comes last scans the table alone -- each thread a contiguous run
-// of m / THREADS entries -- clears `zero` (m entries) and re-arms *done. Next-digit plans (k = 3, 4)
+// bumps *done; the one whose bump comes last scans the table alone -- each wave a contiguous run
+// of 64-quad blocks -- clears `zero` (m entries) and re-arms *done. Next-digit plans (k = 3, 4)
 // scan every table after the first this way: one launch per pass instead of three (rs_scan_reduce
 // + rs_scan_down, each ~5 us at C2, and their launch gaps).
 // Visibility (MI355X_MICROARCH.md, inter-workgroup visibility, the table's first row): the payload
@@ -667,34 +667,51 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
     auto ld = [&](uint32_t quad) {  // 16-B sc1 load (aux 16): L2-served, never a stale L1 line
         return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, quad * 16u, 0, 16));
     };
-    const uint64_t per = ((m + THREADS - 1) / THREADS + 3) & ~(uint64_t)3;
-    const uint32_t beg = (uint32_t)(min(m, (uint64_t)t * per) / 4), end = (uint32_t)(min(m, (uint64_t)t * per + per) / 4);
-    // batches of 12 quads in flight (a latency-bound sweep: m = 20480 at C2 is 20 quads per thread)
-    constexpr uint32_t B = 12;
+    // wave w owns a run of whole 64-quad blocks, lane l quad l of each block: every load and store
+    // instruction covers 1 KiB of consecutive table
+    constexpr uint32_t NW = THREADS / kWave;
+    const uint32_t w = t / kWave, l = lane_id();
+    const uint32_t nq = (uint32_t)(m / 4);
+    const uint32_t per = ((nq + NW - 1) / NW + kWave - 1) & ~(uint32_t)(kWave - 1);
+    const uint32_t qb = min(nq, w * per), qe = min(nq, qb + per);
+    constexpr uint32_t B = 8;  // blocks in flight per wave
     uint32_t s = 0;
-    for (uint32_t i0 = beg; i0 < end; i0 += B) {
+    for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
         u32x4 v[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? ld(i0 + u) : u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t u = 0; u < B; ++u) {
+            const uint32_t qi = b0 + u * kWave + l;
+            v[u] = qi < qe ? ld(qi) : u32x4{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
         for (uint32_t u = 0; u < B; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w;
     }
-    uint32_t tot;
-    uint32_t run = block_excl_scan<THREADS>(s, s_ws, tot);
+    const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan(s), kWave - 1);
+    if (l == 0) s_ws[w] = wsum;
+    __syncthreads();
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < NW; ++x) run += x < w ? s_ws[x] : 0u;
     u32x4 *q = reinterpret_cast<u32x4 *>(table);
-    for (uint32_t i0 = beg; i0 < end; i0 += B) {
+    for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
         u32x4 v[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) v[u] = i0 + u < end ? ld(i0 + u) : u32x4{0u, 0u, 0u, 0u};
+        for (uint32_t u = 0; u < B; ++u) {
+            const uint32_t qi = b0 + u * kWave + l;
+            v[u] = qi < qe ? ld(qi) : u32x4{0u, 0u, 0u, 0u};
+        }
 #pragma unroll
         for (uint32_t u = 0; u < B; ++u) {
+            const uint32_t qs = v[u].x + v[u].y + v[u].z + v[u].w;
+            const uint32_t inc = wave_incl_scan(qs);
             u32x4 o;
-            o.x = run;
-            o.y = run + v[u].x;
+            o.x = run + inc - qs;
+            o.y = o.x + v[u].x;
             o.z = o.y + v[u].y;
             o.w = o.z + v[u].z;
-            run = o.w + v[u].w;
-            if (i0 + u < end) q[i0 + u] = o;
+            const uint32_t qi = b0 + u * kWave + l;
+            if (qi < qe) q[qi] = o;
+            run += __builtin_amdgcn_readlane(inc, kWave - 1);
         }
     }
     u32x4 *z = reinterpret_cast<u32x4 *>(zero);
