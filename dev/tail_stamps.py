@@ -1,5 +1,6 @@
-"""dev/tail_stamps.py -- with a library variant built with -DRS_TAIL_STAMPS (dev/build_variant.sh), time
-the phases of the last pass's tail scan at C2 (s_memrealtime, 100 MHz) from the workspace's tail area."""
+"""dev/tail_stamps.py -- with the stamps variant of the library (dev/build_variant.sh tstamp2 ...), the
+timeline of the last tail-scanned pass at C2 (s_memrealtime, 100 MHz): first workgroup start, last
+workgroup's end of work, tail start, tail end."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "cuda.radixsort_amd"))
 import torch
@@ -10,10 +11,10 @@ rs.gen_uniform(x, 0x5EED)
 y = torch.empty_like(x)
 p = rs.plan(n, k)
 ws = rs.workspace(p.workspace_bytes)
-for rep in range(5):
+for rep in range(6):
     rs.sort_device(x, y, k, ws=ws, plan_=p)
     torch.cuda.synchronize()
-    tail = ws[-256:].view(torch.int32).cpu().numpy().view("uint32")
-    st = [int(tail[8 + 2 * i]) | (int(tail[9 + 2 * i]) << 32) for i in range(4)]
-    print("tail phases (us): sum sweep + wave totals %.2f, scan sweep + stores %.2f, zeroing %.2f" %
-          ((st[1] - st[0]) / 100, (st[2] - st[1]) / 100, (st[3] - st[2]) / 100), flush=True)
+    d = ws[-256:].view(torch.int32).cpu().numpy().view("uint32").astype("int64")
+    t0, tm, ts, te = d[10], d[11], d[8], d[9]
+    print("us from first start: last work end %.2f, tail start %.2f, tail end %.2f" %
+          ((tm - t0) / 100, (ts - t0) / 100, (te - t0) / 100), flush=True)
