@@ -705,6 +705,8 @@ int main(int argc, char **argv) {
         run<8, 1024, 16>(c, "lx pad plain", lx_lines<8, 1024, 16, 32, OC | kPad | kStPlain>, g_shift);
         run<8, 1024, 16>(c, "lib CL rs_scatter_lines<...,3,1>", rs_scatter_lines<8, 1024, 16, 32, false, kDigitShift, 3, 1>, g_shift);
         run<8, 1024, 16>(c, "lx pad hot2", lx_lines<8, 1024, 16, 32, OC | kPad | kHot2>, g_shift);
+        run<8, 1024, 16>(c, "lx pad runs", lx_lines<8, 1024, 16, 32, OC | kPad | kRuns>, g_shift);
+        run<8, 1024, 16>(c, "lx pad runsagg", lx_lines<8, 1024, 16, 32, OC | kPad | kRunsAgg>, g_shift);
         run<8, 1024, 16>(c, "lx pad peer", lx_lines<8, 1024, 16, 32, OC | kPad | kPeer>, g_shift);
         run<8, 1024, 16>(c, "lx pad peerhot", lx_lines<8, 1024, 16, 32, OC | kPad | kPeerHot>, g_shift);
     }
