@@ -229,7 +229,8 @@ Carve carve(const rsort_plan &p, void *ws) {
 // ------------------------------------------------------------------------------ pass pieces
 // Joint pass (pass p of a joint_plan counting for pass p + 1): one workgroup per chunk counts
 // this pass's table and the joint counts; then the chunks of pass p + 1 (its digit groups, or
-// the cut plan). enable: nullptr, or the previous joint pass's flag (kGroupsFixed: no joint count).
+// the cut plan). enable: nullptr, or the previous odd pass's mode: the joint count runs only after
+// whole digit groups (after a cut plan the input is clustered and the count costs more than it saves).
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                        uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
                        uint32_t *pcounts, hipStream_t s, bool zero_joint) {
