@@ -100,6 +100,9 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     // partitions: 4096-key tiles (measured at 2^30 keys into 8 ranges: 1024-thread 16384-key
     // tiles need 4-bit bucket digits, i.e. 15 splitter compares per key, and were 1.3x slower)
     if (k >= 13) return kGeomXL;
+    // keys-only partitions of large inputs: 8192-key tiles of 512 threads (3-bit bucket digits keep
+    // a digit's thread group inside one wave; runs of ~1024 keys per bucket and tile)
+    if (partition && !pairs && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     if (partition || rank == RSORT_RANK_SPLIT) return kGeomSmall;
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
     // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:

@@ -1757,7 +1757,16 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
                     return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
                                                                       PAIRS, kDigitSplit, PAIRS ? 2 : 3>);
             }
+            if constexpr (BITS >= 3 && !PAIRS) {
+                // keys-only partitions of large inputs: 8192-key tiles of 512 threads (kGeomK4's shape)
+                constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
+                if (geom == kGeomK4 && rank == kRankAtomic && aligned16)
+                    return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitSplit, 3>);
+            }
             if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
+            if constexpr (BITS >= 3 && !PAIRS) {
+                if (geom == kGeomK4 && rank != kRankSplit) return scatter_cf<BITS, false, kDigitSplit, kGeomK4>(rank);
+            }
         }
         return nullptr;
     }
