@@ -77,7 +77,24 @@ def parse():
                     help="time the pass primitives in isolation instead (SURVEY 8f row 3) and exit")
     ap.add_argument("--no-group-chunks", action="store_true",
                     help="every pass counts its own histogram (no digit-group chunks)")
+    ap.add_argument("--configs", default="c2,zipf,c4",
+                    help="BASELINE configurations measured after the headline in the same process, "
+                         "reported in the line's `configs` block ('' for none; N=1 only): " + ", ".join(CONFIGS))
+    ap.add_argument("--configs-n", type=int, default=0, help="override every config's key count (tests)")
+    ap.add_argument("--configs-reps", type=int, default=7, help="timed sorts per config (median)")
     return ap.parse_args()
+
+
+# BASELINE.json's other single-GPU configurations (configs[1], configs[3]) and the Zipf keys between
+# them, measured in the same process after the headline (configs[2]) so the driver's run observes them
+CONFIGS = {
+    "c2": {"n": 1 << 26, "k": 4, "dist": "uniform", "pairs": False,
+           "what": "C2 (BASELINE configs[1]): 2^26 uniform u32 keys, k=4"},
+    "zipf": {"n": 1 << 30, "k": 8, "dist": "zipf", "pairs": False,
+             "what": "2^30 Zipf(s=1) u32 keys, k=8 (C4's keys without the payload)"},
+    "c4": {"n": 1 << 30, "k": 8, "dist": "zipf", "pairs": True,
+           "what": "C4 (BASELINE configs[3]): 2^30 Zipf(s=1) u32 keys + u32 payloads (the input index), k=8"},
+}
 
 
 def profile_record(config_key: str):
@@ -221,6 +238,79 @@ def primitives(a, dev):
                       "num_chunks": p.num_chunks, "steps": a.steps, "peak_GBs": HBM_PEAK_GBS}), flush=True)
 
 
+def gen_keys(n, dist, seed, dev):
+    keys = rs.empty_u32(n, dev)
+    if dist == "uniform":
+        rs.gen_uniform(keys, seed)
+    elif dist == "equal":
+        keys.fill_(0x1234567)
+    else:
+        sys.path.insert(0, str(ROOT / "tests"))
+        from _util import zipf_cdf_u32  # the workload's CDF table (data, not the oracle)
+        rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32(), dev), seed)
+    return keys
+
+
+def run_config(name, c, dev, reps, n_override=0):
+    """One BASELINE configuration, device-resident like the headline: ms per sort = the median of
+    `reps` back-to-back sorts, each between two HIP events on the library's stream (torch's current
+    stream); the scatter kernel's average launch time from HIP events around every scatter launch
+    of 3 more sorts (rsort_profile_*); the output checked on the device (sorted, the input's
+    multiset fingerprint)."""
+    n = n_override or c["n"]
+    keys = gen_keys(n, c["dist"], 0x5EED, dev)
+    vals = None
+    if c["pairs"]:
+        vals = rs.empty_u32(n, dev)
+        rs.gen_iota(vals, 0)
+    fp_in = rs.fingerprint(keys, vals)[0]
+    p = rs.plan(n, c["k"], c["pairs"])
+    ws = rs.workspace(p.workspace_bytes, dev)
+    out = rs.empty_u32(n, dev)
+    vout = rs.empty_u32(n, dev) if c["pairs"] else None
+
+    def step():
+        rs.sort_device(keys, out, c["k"], vals_in=vals, vals_out=vout, ws=ws, plan_=p)
+
+    rs.scatter_kernels_used(reset=True)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record()
+    for i in range(reps):
+        step()
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))
+    med = ts[len(ts) // 2]
+    with rs.Profile() as prof:
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+    fp_out, desc = rs.fingerprint(out, vout)
+    sc = prof.times["scatter"]
+    launch_ms = sc["ms"] / max(1, sc["launches"])
+    bpk = 16 if c["pairs"] else 8
+    algo = bpk * sc["keys"] / max(1, sc["launches"])
+    achieved = algo / (launch_ms * 1e-3) / 1e9
+    groups = rs.group_flags(p, ws)
+    res = {"what": c["what"], "keys": n, "k_bits": c["k"], "dist": c["dist"], "pairs": c["pairs"],
+           "ms_per_sort": round(med, 3), "ms_per_sort_min_max": [round(ts[0], 3), round(ts[-1], 3)], "sorts": reps,
+           "Mkeys_per_s": round(n / (med * 1e-3) / 1e6, 1),
+           "scatter": {"avg_launch_ms": round(launch_ms, 4), "bytes_per_key": bpk,
+                       "achieved_GBs": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                       "launches_per_sort": sc["launches"] // 3},
+           "phases_ms_per_sort": {ph: round(prof.times[ph]["ms"] / 3, 4) for ph in ("histogram", "scan", "scatter")},
+           "group_chunk_modes": [("fixed", "groups", "cut")[f] for f in groups] if p.k_bits == 8 else None,
+           "scatter_kernels": rs.scatter_kernels_used(reset=True),
+           "plan_check": rs.plan_check(p, ws),
+           "verified": bool(fp_out == fp_in and desc == 0)}
+    del keys, vals, out, vout, ws
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -262,15 +352,7 @@ def main():
 
     n = a.n
     seed = 0x5EED + rank * n  # one global splitmix stream, block-distributed by index
-    keys = rs.empty_u32(n, dev)
-    if a.dist == "uniform":
-        rs.gen_uniform(keys, seed)
-    elif a.dist == "equal":
-        keys.fill_(0x1234567)
-    else:
-        sys.path.insert(0, str(ROOT / "tests"))
-        from _util import zipf_cdf_u32
-        rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32(), dev), seed)
+    keys = gen_keys(n, a.dist, seed, dev)
     vals = None
     if a.pairs:
         vals = rs.empty_u32(n, dev)
@@ -307,6 +389,7 @@ def main():
         def step():
             rs.sort_device(keys, out, a.k, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
 
+    rs.scatter_kernels_used(reset=True)
     with stdout_to_stderr():  # torch's nccl group connects on its first collective
         for _ in range(a.warmup):
             step()
@@ -366,6 +449,8 @@ def main():
         fp_out, desc = rs.fingerprint(out, vout)
         verified = fp_out == fp_in and desc == 0
     groups = rs.group_flags(p, ws) if not use_dist else None
+    kernels_used = rs.scatter_kernels_used(reset=True)  # what the dispatch launched in these steps
+    probe = rs.lane_order_probe()
 
     # per-kernel: the fused local-sort + scatter pass (the dominant kernel)
     sc = prof.times["scatter"]
@@ -412,8 +497,20 @@ def main():
                "what": "host->host sortByDevice (H2D + sort + D2H, pageable buffers, Parallel7.cu:646-661)"}
         del hout
 
+    configs = None
+    if not use_dist and a.configs.strip():
+        # the other BASELINE configurations, driver-observed: same process, after the headline
+        del keys, vals, out, vout, ws
+        torch.cuda.empty_cache()
+        configs = {}
+        for name in [x.strip() for x in a.configs.split(",") if x.strip()]:
+            configs[name] = run_config(name, CONFIGS[name], dev, a.configs_reps, a.configs_n)
+
     if rank == 0:
         total_keys = n * world * a.steps
+        plain = [k for k in kernels_used if not k.endswith(", 1>")]  # (", 1>": the clustered-input variant)
+        if plain and not use_dist:
+            kernel = plain[-1]
         roof = {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -454,6 +551,13 @@ def main():
                        # fixed chunks with a counted histogram (rsort_group_flags)
                        "group_chunk_modes": ([("fixed", "groups", "cut")[f] for f in groups]
                                              if groups is not None else None),
+                       # the scatter instantiations the library's dispatch launched in the timed
+                       # steps (rsort_scatter_kernels_used), and the ranking the probe allowed
+                       "scatter_kernels": kernels_used,
+                       "lane_order_probe": probe,
+                       "ranking": ("lane-ordered returning LDS adds (kRankAtomic)" if probe == 1 and a.rank == "match"
+                                   else "wave64 ballot peer match (kRankCount)" if a.rank == "match"
+                                   else "k 1-bit splits (kRankSplit)"),
                        "parallelism": "single GPU" if not use_dist else
                        f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'})"},
             "verified": bool(verified),
@@ -461,6 +565,8 @@ def main():
             "phases_ms_per_step": {"histogram": round(hi["ms"] / a.steps, 4), "scan": round(scan["ms"] / a.steps, 4),
                                    "scatter": round(sc["ms"] / a.steps, 4)},
         }
+        if configs:
+            line["configs"] = configs
         if vendor:
             line["vendor"] = vendor
         if e2e:

@@ -400,6 +400,8 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // next-digit counts (k = 3, 4): the same kernel conditions as digit groups
     const bool nextc = next_plan(p) && g_group_chunks.load() != 0 && internal_rank(g_rank_algo.load()) == kRankAtomic &&
                        ((((uintptr_t)kout) | (uintptr_t)c.tmp_k) & 15u) == 0;
+    if (next_plan(p) && !nextc && hipMemsetAsync(c.done, 0, 8, s) != hipSuccess)  // rsort_plan_check: clean
+        return RSORT_ERR_HIP;
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
         const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
@@ -670,6 +672,25 @@ int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flag
     flags[0] = (int)h[0];  // kGroupsFixed / kGroupsWhole / kGroupsCut
     flags[1] = (int)h[1];
     return RSORT_OK;
+}
+
+int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream) {
+    if (!plan || !flags || !d_workspace) return RSORT_ERR_ARG;
+    int st = check_plan(plan);
+    if (st) return st;
+    *flags = 0;
+    if (!next_plan(*plan) || plan->n == 0) return RSORT_OK;
+    const Carve c = carve(*plan, const_cast<void *>(d_workspace));
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h = 0;
+    if (hipMemcpyAsync(&h, c.done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    *flags = h ? 1 : 0;
+    return RSORT_OK;
+}
+
+size_t rsort_scatter_kernels_used(char *buf, size_t len, int reset) {
+    return scatter_kernels_used(buf, len, reset);
 }
 
 int rsort_lane_order_probe(void) {

@@ -193,5 +193,11 @@ hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t
 hipError_t launch_widen(const uint32_t *in, unsigned long long *out, uint32_t n, hipStream_t s);
 // Resident scatter workgroups per CU (occupancy query), 0 on error.
 int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmode = kDigitShift);
+// Names of the scatter kernel instantiations launched since the last reset, ';'-joined into buf
+// (truncated to len - 1 characters); returns the full length. reset != 0 clears the record.
+size_t scatter_kernels_used(char *buf, size_t len, int reset);
+// Workspace check words (next-digit plans): done[kDoneErr] is set when a tail scan found a table
+// whose total is not n even after an agent-scope acquire and a second sweep.
+constexpr uint32_t kDoneErr = 1;
 
 }  // namespace rsort

@@ -18,22 +18,76 @@
 // and each digit's output run continues where the previous tile of the same workgroup
 // stopped (partial cache lines complete inside one CU's L2 before write-back).
 //
-// Local rank (the "block-local 1-bit split sort" of the north star), two interchangeable
-// algorithms giving the same unique stable order:
-//   RANK_MATCH  per key: k wave64 ballots build the mask of lanes holding the same digit;
-//               rank-in-wave = popcount(mask & lanes-below) + a per-wave LDS digit counter
-//               bumped by ONE lane with a returning ds_add (no serial dependence between
-//               slots); then a block scan of the W x R counters gives every key's tile rank.
-//   RANK_SPLIT  k successive stable 1-bit splits (the reference's P5:79-159 / P7:79-191
-//               algorithm), each a ballot/popcount block scan + one LDS permutation.
+// Local rank (the "block-local 1-bit split sort" of the north star), three interchangeable
+// algorithms giving the same unique stable order (public rsort_rank_algo -> internal RankAlgo):
+//   RSORT_RANK_MATCH (default) -> kRankAtomic: count first (per-wave LDS digit counters), scan
+//               them into tile positions, then ONE returning ds_add per key: gfx950 serves the
+//               lanes of one ds_add_rtn_u32 that hit the same address in ascending lane order,
+//               so the returned value IS the key's stable position (rank_add / rank_add_hot;
+//               rs_lane_order_probe re-checks the premise once per device and the library falls
+//               back to kRankCount when it fails).
+//   RSORT_RANK_BALLOT -> kRankCount: the same count-first scheme with a wave64 ballot peer match
+//               (k ballots build the mask of lanes holding the same digit; rank-in-wave =
+//               popcount(mask & lanes-below) + the per-wave counter bumped by one lane).
+//   RSORT_RANK_SPLIT -> kRankSplit: k successive stable 1-bit splits (the reference's
+//               P5:79-159 / P7:79-191 algorithm), each a ballot/popcount block scan + one LDS
+//               permutation.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
 #include <mutex>
+#include <string>
+#include <vector>
 
 #include "rsort_internal.hpp"
 
 namespace rsort {
+
+// ------------------------------------------------------------------------------ kernel names
+// Which scatter kernels a sort actually launched (rsort_scatter_kernels_used, bench.py's line):
+// every kernel pointer the dispatch below hands out goes through reg_lines<...>() / reg_scatter<...>(),
+// which
+// records the instantiation's name (its template arguments) once; launch_scatter notes the pointers
+// it launches.
+namespace {
+std::mutex g_kn_mu;
+std::vector<std::pair<const void *, std::string>> g_kn_names;  // every registered kernel
+std::vector<const void *> g_kn_used;                           // launched since the last reset
+
+void register_kernel(const void *fn, const char *name) {
+    std::lock_guard<std::mutex> g(g_kn_mu);
+    g_kn_names.emplace_back(fn, std::string(name));
+}
+
+void note_used(const void *fn) {
+    std::lock_guard<std::mutex> g(g_kn_mu);
+    for (const void *u : g_kn_used)
+        if (u == fn) return;
+    g_kn_used.push_back(fn);
+}
+}  // namespace
+
+size_t scatter_kernels_used(char *buf, size_t len, int reset) {
+    std::lock_guard<std::mutex> g(g_kn_mu);
+    std::string out;
+    for (const void *u : g_kn_used) {
+        std::string nm = "?";
+        for (auto &kv : g_kn_names)
+            if (kv.first == u) nm = kv.second;
+        if (!out.empty()) out += ";";
+        out += nm;
+    }
+    if (reset) g_kn_used.clear();
+    if (buf && len > 0) {
+        const size_t m = std::min(len - 1, out.size());
+        memcpy(buf, out.data(), m);
+        buf[m] = '\0';
+    }
+    return out.size();
+}
 
 
 // ------------------------------------------------------------------------------ helpers
@@ -540,7 +594,10 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
     // pass's scatter, finished before this launch)
     for (uint64_t i = (uint64_t)blockIdx.x * kScanThreads + threadIdx.x; i < a.zero_n; i += (uint64_t)gridDim.x * kScanThreads)
         a.zero[i] = 0u;
-    if (a.done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.done = 0u;
+    if (a.done != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.done[0] = 0u;         // the tail-scan counter
+        a.done[kDoneErr] = 0u;  // its check word (tail_scan)
+    }
     const uint64_t base = (uint64_t)blockIdx.x * kScanSegment + (uint64_t)threadIdx.x * kScanPerThread;
     uint32_t s = 0;
     if (a.group_flag != nullptr && *a.group_flag == kGroupsCut) {
@@ -647,10 +704,14 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 // waits for them before its workgroup's one counter add, the last adder learns it from the value
 // its add returns, and every load of the table is a 16-B sc1 load -- so neither a release fence
 // per workgroup (a `buffer_wbl2` wrote back the default-policy output held in L2 and doubled the
-// C2 pass time) nor an acquire fence (~1.7 us) is needed. All threads must call it.
+// C2 pass time) nor an acquire fence (~1.7 us) is needed. The table counts every key of the pass
+// exactly once, so its total must be `expect` (= n): the sum sweep checks that, and on a mismatch
+// (a late or stale line -- never observed) the workgroup takes the agent-scope acquire fence and
+// sums again; a second mismatch sets done[kDoneErr] (rsort_plan_check) -- so a visibility failure
+// is repaired or reported, never silent. All threads must call it.
 template <int THREADS>
 __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t *done, uint32_t *s_ws,
-                          uint32_t *s_flag) {
+                          uint32_t *s_flag, uint32_t expect) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t t = threadIdx.x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's adds have been performed
@@ -675,23 +736,36 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
     const uint32_t per = ((nq + NW - 1) / NW + kWave - 1) & ~(uint32_t)(kWave - 1);
     const uint32_t qb = min(nq, w * per), qe = min(nq, qb + per);
     constexpr uint32_t B = 8;  // blocks in flight per wave
-    uint32_t s = 0;
-    for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
-        u32x4 v[B];
+    uint32_t run = 0, total = 0;
+    for (int attempt = 0;; ++attempt) {
+        uint32_t s = 0;
+        for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
+            u32x4 v[B];
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) {
-            const uint32_t qi = b0 + u * kWave + l;
-            v[u] = qi < qe ? ld(qi) : u32x4{0u, 0u, 0u, 0u};
+            for (uint32_t u = 0; u < B; ++u) {
+                const uint32_t qi = b0 + u * kWave + l;
+                v[u] = qi < qe ? ld(qi) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < B; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w;
         }
+        const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan(s), kWave - 1);
+        if (l == 0) s_ws[w] = wsum;
+        __syncthreads();
+        run = 0;
+        total = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < B; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w;
+        for (uint32_t x = 0; x < NW; ++x) {
+            const uint32_t y = s_ws[x];
+            run += x < w ? y : 0u;
+            total += y;
+        }
+        // (total is the same in every thread: the branches below are uniform)
+        if (total == expect || attempt == 1) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __syncthreads();  // every wave has read s_ws before it is written again
     }
-    const uint32_t wsum = __builtin_amdgcn_readlane(wave_incl_scan(s), kWave - 1);
-    if (l == 0) s_ws[w] = wsum;
-    __syncthreads();
-    uint32_t run = 0;
-#pragma unroll
-    for (uint32_t x = 0; x < NW; ++x) run += x < w ? s_ws[x] : 0u;
+    if (total != expect && t == 0) atomicOr(&done[kDoneErr], 1u);
     u32x4 *q = reinterpret_cast<u32x4 *>(table);
     for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
         u32x4 v[B];
@@ -1574,7 +1648,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
             // the last workgroup scans the next pass's table (no scan launches between passes)
             if (a.done != nullptr) {
                 __shared__ uint32_t s_last;
-                tail_scan<THREADS>(a.next_table, (uint64_t)R * a.num_chunks, a.tail_zero, a.done, s_ws, &s_last);
+                tail_scan<THREADS>(a.next_table, (uint64_t)R * a.num_chunks, a.tail_zero, a.done, s_ws, &s_last,
+                                   (uint32_t)a.n);
             }
         }
     }
@@ -1705,6 +1780,35 @@ __global__ void rs_gen_iota(uint32_t *out, uint64_t n, uint32_t base) {
 }
 
 // ------------------------------------------------------------------------------ dispatch
+// Kernel pointers with their names recorded (rsort_scatter_kernels_used).
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
+static void *reg_lines() {
+    void *fn = reinterpret_cast<void *>(&rs_scatter_lines<BITS, THREADS, KPT, G, PAIRS, DMODE, NT, CL>);
+    static const bool once = [fn] {
+        char nm[96];
+        snprintf(nm, sizeof nm, "rs_scatter_lines<%d, %d, %d, %d, %s, %d, %d, %d>", BITS, THREADS, KPT, G,
+                 PAIRS ? "true" : "false", DMODE, NT, CL);
+        register_kernel(fn, nm);
+        return true;
+    }();
+    (void)once;
+    return fn;
+}
+
+template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW>
+static void *reg_scatter() {
+    void *fn = reinterpret_cast<void *>(&rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, DMODE, MINW>);
+    static const bool once = [fn] {
+        char nm[96];
+        snprintf(nm, sizeof nm, "rs_scatter<%d, %d, %d, %s, %d, %d, %d>", BITS, THREADS, KPT, PAIRS ? "true" : "false",
+                 RANK, DMODE, MINW);
+        register_kernel(fn, nm);
+        return true;
+    }();
+    (void)once;
+    return fn;
+}
+
 template <int BITS>
 static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (dmode == kDigitSplit) {
@@ -1727,14 +1831,16 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
 }
 
 #ifndef RSORT_LAB_LITE  // dev labs that instantiate their own variants skip the library's set
-// The compiled scatter kernels. "match" (the default rank algorithm) is the count-first peer
-// match (kRankCount); "split" is the reference's 1-bit split sort. Geometries per kGeomShape.
+// The compiled scatter kernels. "match" (the default public rank algorithm) runs kRankAtomic, the
+// lane-ordered returning LDS add per key (kRankCount, the ballot peer match, where the lane-order
+// probe fails or RSORT_RANK_BALLOT asks for it); "split" is the reference's 1-bit split sort.
+// Geometries per kGeomShape.
 template <int BITS, bool PAIRS, int RANK, int DMODE, int G>
 static void *scatter_fn() {
     constexpr int TH = kGeomShape[G].threads;
     constexpr int KPT = kGeomShape[G].kpt;
     constexpr int MINW = (G == kGeomK4) ? 4 : 0;
-    return reinterpret_cast<void *>(&rs_scatter<BITS, TH, KPT, PAIRS, RANK, DMODE, MINW>);
+    return reg_scatter<BITS, TH, KPT, PAIRS, RANK, DMODE, MINW>();
 }
 
 // count-first ranking: rank = kRankAtomic (lane-ordered LDS adds) or kRankCount (ballots)
@@ -1754,14 +1860,14 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
                 // (a digit's thread group must fit one wave: BITS >= 2)
                 constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
                 if (geom == kGeomSmall && rank == kRankAtomic && aligned16)
-                    return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
-                                                                      PAIRS, kDigitSplit, PAIRS ? 2 : 3>);
+                    return reg_lines<BITS, TH, KP, PAIRS ? kLineKeysPairs : kLineKeys,
+                                                                      PAIRS, kDigitSplit, PAIRS ? 2 : 3>();
             }
             if constexpr (BITS >= 3 && !PAIRS) {
                 // keys-only partitions of large inputs: 8192-key tiles of 512 threads (kGeomK4's shape)
                 constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
                 if (geom == kGeomK4 && rank == kRankAtomic && aligned16)
-                    return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitSplit, 3>);
+                    return reg_lines<BITS, TH, KP, kLineKeys, false, kDigitSplit, 3>();
             }
             if (geom == kGeomSmall && rank != kRankSplit) return scatter_cf<BITS, PAIRS, kDigitSplit, kGeomSmall>(rank);
             if constexpr (BITS >= 3 && !PAIRS) {
@@ -1780,7 +1886,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
             // aligned outputs, like kGeomLines)
             constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
             if (rank == kRankAtomic && aligned16)
-                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, 3>);
+                return reg_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, 3>();
         }
         return scatter_cf<BITS, PAIRS, kDigitShift, kGeomSmall>(rank);
     }
@@ -1792,9 +1898,9 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
         if (geom == GL) {
             if (rank == kRankAtomic && aligned16)
-                return reinterpret_cast<void *>(&rs_scatter_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
+                return reg_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
                                                                   PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
-                                                                  kDigitShift, PAIRS ? 2 : 3>);
+                                                                  kDigitShift, PAIRS ? 2 : 3>();
             return scatter_cf<BITS, PAIRS, kDigitShift, GL>(rank);
         }
     }
@@ -1963,20 +2069,22 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomSmall &&
         rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
         constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
-        fn = bits == 3 ? reinterpret_cast<void *>(&rs_scatter_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>)
-                       : reinterpret_cast<void *>(&rs_scatter_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>);
+        fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
+                       : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
     }
     // clustered-input variants of the k = 8 line kernels (rank_add_hot): both kernels are launched,
     // the device-side flag *cl_select picks the one that works (the other leaves at once: ~3 us)
     void *cl = nullptr;
     if (a.cl_select != nullptr) {
         if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3>))
-            cl = reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>);
+            cl = reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
         else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2>))
-            cl = reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>);
+            cl = reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>();
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
+    note_used(fn);
+    if (cl != nullptr) note_used(cl);
     void *args[] = {&copy};
     hipError_t e = hipLaunchKernel(fn, dim3(a.num_chunks), dim3(kGeomShape[geom].threads), args, 0, s);
     if (e != hipSuccess || cl == nullptr) return e;

@@ -46,12 +46,16 @@ std::atomic<int64_t> g_piece{kMaxPiece};  // rsort_set_exchange_piece (tests for
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// step 1's all-gathered words per rank: key count, values flags, local status
+constexpr size_t kNWords = 3;
+
 struct MultiCarve {
     uint32_t *part_k, *part_v;
-    uint64_t *n_send, *n_all;      // [2], [world][2]: key count, values flags
-    uint64_t *c_send, *c_all;      // [kMaxBuckets + 1], [world][kMaxBuckets + 1]
+    uint64_t *n_send, *n_all;      // [kNWords], [world][kNWords]
+    uint64_t *c_send, *c_all;      // [kMaxBuckets + 2], [world][kMaxBuckets + 2]: counts, capacity, status
     uint32_t *starts;              // [kMaxBuckets + 1]
-    uint32_t *samp_send, *samp_all;  // [kSampleBudget], [world][kSampleBudget]
+    uint32_t *samp_send, *samp_all;  // [kSampleBudget + 1], [world][...]: the sample row + the status
+    size_t control_bytes;          // the buffers above part_k
     void *sub;                     // partition, sample sort and local sort, in turn
     size_t sub_bytes;
 };
@@ -76,15 +80,18 @@ size_t multi_bytes(int64_t n, int64_t cap, int k, int pairs, int world, MultiCar
         return (char *)base + o;
     };
     MultiCarve m{};
+    // the collectives' small buffers first: a rank whose workspace is too small for the rest still
+    // takes part in them (with its error status, so every rank returns it together)
+    m.n_send = (uint64_t *)take(kNWords * 8);
+    m.n_all = (uint64_t *)take((size_t)kMaxRanks * kNWords * 8);
+    m.c_send = (uint64_t *)take((size_t)(kMaxBuckets + 2) * 8);
+    m.c_all = (uint64_t *)take((size_t)kMaxRanks * (kMaxBuckets + 2) * 8);
+    m.starts = (uint32_t *)take((size_t)(kMaxBuckets + 1) * 4);
+    m.samp_send = (uint32_t *)take((size_t)(kSampleBudget + 1) * 4);
+    m.samp_all = (uint32_t *)take((size_t)world * (kSampleBudget + 1) * 4);
+    m.control_bytes = off;
     m.part_k = (uint32_t *)take((size_t)n * 4);
     m.part_v = pairs ? (uint32_t *)take((size_t)n * 4) : nullptr;
-    m.n_send = (uint64_t *)take(16);
-    m.n_all = (uint64_t *)take((size_t)kMaxRanks * 16);
-    m.c_send = (uint64_t *)take((size_t)(kMaxBuckets + 1) * 8);
-    m.c_all = (uint64_t *)take((size_t)kMaxRanks * (kMaxBuckets + 1) * 8);
-    m.starts = (uint32_t *)take((size_t)(kMaxBuckets + 1) * 4);
-    m.samp_send = (uint32_t *)take((size_t)kSampleBudget * 4);
-    m.samp_all = (uint32_t *)take((size_t)world * kSampleBudget * 4);
     m.sub_bytes = sub_bytes(n, cap, k, pairs, world);
     m.sub = take(m.sub_bytes);
     if (mc) *mc = m;
@@ -225,87 +232,137 @@ int d2h(void *h, const void *d, size_t bytes, hipStream_t s) {
     return hip_st(hipStreamSynchronize(s));
 }
 
+// Exchange rounds for messages of up to max_message keys with at most `limit` keys per message:
+// equal pieces, a multiple of 64 keys (256-B aligned message starts) and never above the limit
+// (rounded down, so a limit that is not a multiple of 64 still holds).
+void exchange_rounds(int64_t max_message, int64_t limit, int64_t *rounds, int64_t *piece) {
+    *rounds = 0;
+    *piece = 0;
+    if (max_message <= 0) return;
+    limit = std::max<int64_t>(limit, 64);
+    const int64_t r0 = (max_message + limit - 1) / limit;      // rounds at the limit
+    int64_t p = (max_message + r0 - 1) / r0;                    // equal pieces, <= limit
+    p = std::max<int64_t>(64, p / 64 * 64);
+    *piece = p;
+    *rounds = (max_message + p - 1) / p;
+}
+
 int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32_t *d_keys_out, uint32_t *d_vals_out,
                int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits, const rsort_transport *tr,
                void *d_workspace, size_t workspace_bytes, hipStream_t s) {
-    if (k_bits < kMinBits || k_bits > kMaxBits) return RSORT_ERR_BITS;
-    if (n < 0 || n >= ((int64_t)1 << 32) || capacity < 0 || capacity >= ((int64_t)1 << 32)) return RSORT_ERR_SIZE;
-    if (!tr || !tr->allgather || !tr->exchange || !out_n || !out_offset || !d_workspace) return RSORT_ERR_ARG;
+    // What every collective needs: a transport, this rank's place in it and the small control
+    // buffers. Without them a rank cannot even tell its peers it failed (caller error).
+    if (!tr || !tr->allgather || !tr->exchange || !d_workspace) return RSORT_ERR_ARG;
+    const int world = tr->world, me = tr->rank;
+    if (world < 1 || world > kMaxRanks || me < 0 || me >= world) return RSORT_ERR_ARG;
+    const bool sizes_ok = n >= 0 && n < ((int64_t)1 << 32) && capacity >= 0 && capacity < ((int64_t)1 << 32);
     // a rank sorts pairs when it passes values or a values output (a rank with no keys may pass
     // an empty, NULL values input); the ranks agree on it in step 1
     const int pairs = (d_vals != nullptr || d_vals_out != nullptr) ? 1 : 0;
-    if ((n > 0 && !d_keys) || (capacity > 0 && !d_keys_out)) return RSORT_ERR_ARG;
-    const int world = tr->world, me = tr->rank;
-    if (world < 1 || world > kMaxRanks || me < 0 || me >= world) return RSORT_ERR_ARG;
     MultiCarve m;
-    if (workspace_bytes < multi_bytes(n, capacity, k_bits, pairs, world, &m, d_workspace)) return RSORT_ERR_WORKSPACE;
+    const size_t need = multi_bytes(sizes_ok ? n : 0, sizes_ok ? capacity : 0, k_bits, pairs, world, &m, d_workspace);
+    if (workspace_bytes < m.control_bytes) return RSORT_ERR_WORKSPACE;
+    // Every other local failure is carried to the peers in the next all-gather (a status word per
+    // rank) and returned by every rank together -- the lowest rank's status first -- instead of
+    // leaving the peers waiting in a collective this rank never joins (RCCL has no timeout).
+    int local = RSORT_OK;
+    if (k_bits < kMinBits || k_bits > kMaxBits) local = RSORT_ERR_BITS;
+    else if (!sizes_ok) local = RSORT_ERR_SIZE;
+    else if (!out_n || !out_offset || (n > 0 && !d_keys) || (capacity > 0 && !d_keys_out)) local = RSORT_ERR_ARG;
+    else if (workspace_bytes < need) local = RSORT_ERR_WORKSPACE;
+    if (local != RSORT_OK) n = 0;  // (nothing below reads the keys of a failed rank)
     int st;
+    auto first_status = [&](const uint64_t *words, size_t stride, size_t at) {
+        for (int r = 0; r < world; ++r)
+            if (words[(size_t)r * stride + at] != 0) return (int)words[(size_t)r * stride + at];
+        return (int)RSORT_OK;
+    };
 
-    // 1. key counts and value flags -> sampling plan; a values mismatch between ranks is an
-    //    argument error on every rank (all see the same flags)
-    const uint64_t mine[2] = {(uint64_t)n, (uint64_t)(pairs | (d_vals ? 2 : 0) | (d_vals_out ? 4 : 0))};
-    if (hipMemcpyAsync(m.n_send, mine, 16, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
-    if ((st = tr->allgather(tr->ctx, m.n_send, m.n_all, 16, s))) return st;
-    uint64_t nf[2 * kMaxRanks];
-    if ((st = d2h(nf, m.n_all, (size_t)world * 16, s))) return st;
+    // 1. key counts, value flags and statuses -> sampling plan; a values mismatch between ranks is
+    //    an argument error on every rank (all see the same flags)
+    const uint64_t mine[kNWords] = {(uint64_t)n, (uint64_t)(pairs | (d_vals ? 2 : 0) | (d_vals_out ? 4 : 0)),
+                                    (uint64_t)local};
+    if (hipMemcpyAsync(m.n_send, mine, sizeof(mine), hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
+    if ((st = tr->allgather(tr->ctx, m.n_send, m.n_all, sizeof(mine), s))) return st;
+    uint64_t nf[kNWords * kMaxRanks];
+    if ((st = d2h(nf, m.n_all, (size_t)world * sizeof(mine), s))) return st;
+    if ((st = first_status(nf, kNWords, 2))) return st;
     int64_t n_all[kMaxRanks];
     bool any_pairs = false, bad = false;
     for (int r = 0; r < world; ++r) {
-        n_all[r] = (int64_t)nf[2 * r];
-        any_pairs |= (nf[2 * r + 1] & 1) != 0;
+        n_all[r] = (int64_t)nf[kNWords * r];
+        any_pairs |= (nf[kNWords * r + 1] & 1) != 0;
     }
     for (int r = 0; r < world && any_pairs; ++r)
-        bad |= !(nf[2 * r + 1] & 4) || (n_all[r] > 0 && !(nf[2 * r + 1] & 2));
+        bad |= !(nf[kNWords * r + 1] & 4) || (n_all[r] > 0 && !(nf[kNWords * r + 1] & 2));
     if (bad) return RSORT_ERR_ARG;
     rsort_sample_plan sp;
     if ((st = rsort_multi_sample_plan(world, n_all, samples_per_rank(world), &sp))) return st;
-
-    // 2. sample, gather, sort on the device, read the quantile keys
     if (sp.row_len > kSampleBudget) return RSORT_ERR_ARG;  // cannot happen: budget / world per rank
+
+    // 2. sample (+ this rank's status in the row's last word), gather, sort on the device, read
+    //    the quantile keys
+    const size_t row = (size_t)sp.row_len + 1;
     if (launch_sample(d_keys, (uint64_t)n, (uint64_t)sp.stride, (uint64_t)sp.count[me], (uint64_t)sp.row_len,
                       m.samp_send, s) != hipSuccess)
-        return RSORT_ERR_HIP;
-    if ((st = tr->allgather(tr->ctx, m.samp_send, m.samp_all, (size_t)sp.row_len * 4, s))) return st;
-    uint32_t q[kMaxRanks] = {0};
-    if (world > 1 && sp.total > 0) {
-        const int64_t ns = (int64_t)world * sp.row_len;
-        if ((st = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s))) return st;
-        for (int i = 1; i < world; ++i)
-            if (hipMemcpyAsync(&q[i - 1], m.samp_all + rsort_multi_quantile_index(&sp, i), 4, hipMemcpyDeviceToHost,
-                               s) != hipSuccess)
+        local = RSORT_ERR_HIP;
+    const uint32_t lst = (uint32_t)local;
+    if (hipMemcpyAsync(m.samp_send + sp.row_len, &lst, 4, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
+    if ((st = tr->allgather(tr->ctx, m.samp_send, m.samp_all, row * 4, s))) return st;
+    {
+        uint32_t sts[kMaxRanks];
+        for (int r = 0; r < world; ++r)
+            if (hipMemcpyAsync(&sts[r], m.samp_all + (size_t)r * row + sp.row_len, 4, hipMemcpyDeviceToHost, s) !=
+                hipSuccess)
                 return RSORT_ERR_HIP;
         if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+        for (int r = 0; r < world; ++r)
+            if (sts[r]) return (int)sts[r];
+    }
+    uint32_t q[kMaxRanks] = {0};
+    if (world > 1 && sp.total > 0) {
+        // the rows (each followed by its status word) sorted as one array: the status words are 0
+        // and sort first, so the quantile positions move up by world
+        const int64_t ns = (int64_t)world * (int64_t)row;
+        local = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s);
+        for (int i = 1; i < world && !local; ++i)
+            if (hipMemcpyAsync(&q[i - 1], m.samp_all + world + rsort_multi_quantile_index(&sp, i), 4,
+                               hipMemcpyDeviceToHost, s) != hipSuccess)
+                local = RSORT_ERR_HIP;
+        if (!local && hipStreamSynchronize(s) != hipSuccess) local = RSORT_ERR_HIP;
     }
     rsort_multi_splitters spl;
-    if ((st = rsort_multi_splitters_make(world, q, &spl))) return st;
+    if ((st = rsort_multi_splitters_make(world, q, &spl))) return st;  // pure, identical on every rank
 
     // 3. stable partition into the splitters' buckets
     const int buckets = spl.nsplit + 1;
-    if (buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;
-    if ((st = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, spl.split, buckets, m.starts, m.sub,
-                                     m.sub_bytes, s)))
-        return st;
-    uint32_t starts[kMaxBuckets + 1];
-    if ((st = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s))) return st;
+    if (buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;  // pure: the same on every rank
+    uint32_t starts[kMaxBuckets + 1] = {0};
+    if (!local)
+        local = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, spl.split, buckets, m.starts, m.sub,
+                                       m.sub_bytes, s);
+    if (!local) local = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s);
 
-    // 4. count matrix + capacities -> exchange plan (the same on every rank)
-    uint64_t row[kMaxBuckets + 1];
-    for (int b = 0; b < buckets; ++b) row[b] = (uint64_t)(starts[b + 1] - starts[b]);
-    row[buckets] = (uint64_t)capacity;
-    const size_t row_bytes = (size_t)(buckets + 1) * 8;
-    if (hipMemcpyAsync(m.c_send, row, row_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
+    // 4. count matrix + capacities + statuses -> exchange plan (the same on every rank)
+    uint64_t rowc[kMaxBuckets + 2];
+    for (int b = 0; b < buckets; ++b) rowc[b] = local ? 0u : (uint64_t)(starts[b + 1] - starts[b]);
+    rowc[buckets] = (uint64_t)capacity;
+    rowc[buckets + 1] = (uint64_t)local;
+    const size_t row_bytes = (size_t)(buckets + 2) * 8;
+    if (hipMemcpyAsync(m.c_send, rowc, row_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
     if ((st = tr->allgather(tr->ctx, m.c_send, m.c_all, row_bytes, s))) return st;
-    uint64_t all[kMaxRanks * (kMaxBuckets + 1)];
+    uint64_t all[kMaxRanks * (kMaxBuckets + 2)];
     if ((st = d2h(all, m.c_all, (size_t)world * row_bytes, s))) return st;
+    if ((st = first_status(all, (size_t)buckets + 2, (size_t)buckets + 1))) return st;
     int64_t counts[kMaxRanks * kMaxBuckets], caps[kMaxRanks];
     for (int r = 0; r < world; ++r) {
-        for (int b = 0; b < buckets; ++b) counts[r * buckets + b] = (int64_t)all[r * (buckets + 1) + b];
-        caps[r] = (int64_t)all[r * (buckets + 1) + buckets];
+        for (int b = 0; b < buckets; ++b) counts[r * buckets + b] = (int64_t)all[r * (buckets + 2) + b];
+        caps[r] = (int64_t)all[r * (buckets + 2) + buckets];
     }
     rsort_exchange_plan xp;
     if ((st = rsort_multi_exchange_plan(world, me, buckets, counts, &spl, caps, &xp))) return st;
 
-    // 5. the exchange: own range by a device copy, the rest in equal rounds of <= kMaxPiece keys
+    // 5. the exchange: own range by a device copy, the rest in equal rounds of <= the piece limit
     if (xp.send_cnt[me] != xp.recv_cnt[me]) return RSORT_ERR_ARG;
     if (xp.send_cnt[me] > 0) {
         if (hipMemcpyAsync(d_keys_out + xp.recv_off[me], m.part_k + xp.send_off[me], (size_t)xp.send_cnt[me] * 4,
@@ -315,9 +372,8 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
                                     (size_t)xp.send_cnt[me] * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
             return RSORT_ERR_HIP;
     }
-    const int64_t maxp = g_piece.load();
-    const int64_t rounds = xp.max_message > 0 ? (xp.max_message + maxp - 1) / maxp : 0;
-    const int64_t piece = rounds > 0 ? ((xp.max_message + rounds - 1) / rounds + 63) / 64 * 64 : 0;
+    int64_t rounds = 0, piece = 0;
+    exchange_rounds(xp.max_message, g_piece.load(), &rounds, &piece);
     for (int64_t rd = 0; rd < rounds; ++rd) {
         for (int arr = 0; arr < (pairs ? 2 : 1); ++arr) {
             uint32_t *src = arr ? m.part_v : m.part_k;
@@ -336,7 +392,7 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         }
     }
 
-    // 6. local sort of what arrived, in place
+    // 6. local sort of what arrived, in place (no collective follows: a failure here is this rank's)
     if (xp.n_recv > 0) {
         rsort_plan p;
         if ((st = rsort_plan_make(xp.n_recv, k_bits, pairs, 0, &p))) return st;

@@ -79,6 +79,17 @@ class GpuOps:
         return keys, vals
 
 
+def exchange_rounds(max_message: int, limit: int) -> tuple[int, int]:
+    """(rounds, piece) for messages of up to max_message keys, <= limit keys each: equal pieces
+    of a multiple of 64 keys, rounded down (rsort_multi.cpp exchange_rounds)."""
+    if max_message <= 0:
+        return 0, 0
+    limit = max(limit, 64)
+    r0 = -(-max_message // limit)
+    piece = max(64, (-(-max_message // r0)) // 64 * 64)
+    return -(-max_message // piece), piece
+
+
 def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, capacity=None):
     """Sort the union of every rank's `keys` (and `vals`); return this rank's slice of the
     global sorted order as (keys, vals, global_offset).
@@ -131,8 +142,7 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, capacity=None):
     recv_off, recv_cnt = list(xp.recv_off)[:world], list(xp.recv_cnt)[:world]
     rk = torch.empty(xp.n_recv, dtype=keys.dtype, device=dev)
     rv = torch.empty(xp.n_recv, dtype=vals.dtype, device=dev) if vals is not None else None
-    rounds = -(-xp.max_message // MAX_PIECE) if xp.max_message > 0 else 0
-    piece = (-(-xp.max_message // rounds) + 63) // 64 * 64 if rounds else 0
+    rounds, piece = exchange_rounds(xp.max_message, MAX_PIECE)
     for src, dst in ((pk, rk), (pv, rv)):
         if src is None:
             continue

@@ -149,6 +149,8 @@ SIGNATURES = {
     "rsort_get_group_chunks": ([], _int),
     "rsort_group_flags": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_lane_order_probe": ([], _int),
+    "rsort_plan_check": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
+    "rsort_scatter_kernels_used": ([ctypes.c_char_p, _sz, _int], _sz),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
     "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
@@ -331,6 +333,24 @@ def group_flags(p: Plan, ws, stream=None) -> list[int]:
     flags = (ctypes.c_int * 2)()
     _check(_lib().rsort_group_flags(ctypes.byref(p), _ptr(ws), flags, _stream(stream)), "rsort_group_flags")
     return [int(flags[0]), int(flags[1])]
+
+
+def plan_check(p: Plan, ws, stream=None) -> int:
+    """The on-device self-checks of the last sort with plan `p` and workspace `ws`
+    (rsort_plan_check; synchronises the stream): 0 = all passed."""
+    f = ctypes.c_int()
+    _check(_lib().rsort_plan_check(ctypes.byref(p), _ptr(ws), ctypes.byref(f), _stream(stream)), "rsort_plan_check")
+    return int(f.value)
+
+
+def scatter_kernels_used(reset: bool = False) -> list[str]:
+    """The scatter kernel instantiations launched since the last reset (rsort_scatter_kernels_used):
+    what actually ran, from the library's own dispatch."""
+    n = int(_lib().rsort_scatter_kernels_used(None, 0, 0))
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib().rsort_scatter_kernels_used(buf, n + 1, 1 if reset else 0)
+    s = buf.value.decode()
+    return s.split(";") if s else []
 
 
 def pass_histogram(p: Plan, keys, shift, table, stream=None):

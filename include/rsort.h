@@ -183,6 +183,16 @@ RSORT_API int rsort_get_group_chunks(void);
  * without them). Synchronises the stream. */
 RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
                                 void *stream);
+/* After a sort with `plan` and `d_workspace` has completed on `stream`: *flags = 0 when every
+ * on-device self-check of that sort passed; bit 0 = a k = 3, 4 tail scan found a next-pass table
+ * whose total was not n even after an acquire fence and a second sweep (the sort's output is then
+ * not trustworthy). Synchronises the stream. */
+RSORT_API int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream);
+/* The scatter kernel instantiations this library has launched since the last reset, ';'-joined
+ * into buf (at most len - 1 characters and a NUL); returns the full length. reset != 0 clears the
+ * record. A k = 8 digit-group sort launches a plain and a clustered-input kernel for each pass
+ * after the first (the device picks one, the other leaves at once): both are listed. */
+RSORT_API size_t rsort_scatter_kernels_used(char *buf, size_t len, int reset);
 /* 1 if the current device's LDS returns same-address atomic adds in lane order (the default
  * ranking relies on it and falls back to ballots otherwise), 0 if not, < 0 on error. The
  * probe runs once per device (a few microseconds) and is cached. */
@@ -294,7 +304,14 @@ RSORT_API int rsort_multi_exchange_plan(int world, int me, int buckets, const in
  * times (counts are needed on the host).
  * capacity: room in d_keys_out / d_vals_out. RSORT_ERR_CAPACITY when ANY rank would receive more
  * than its capacity: every rank returns it, before any key moves (balanced output needs about
- * total / world plus the sampling error, ~0.1 %). Up to RSORT_MAX_RANKS ranks. */
+ * total / world plus the sampling error, ~0.1 %). Up to RSORT_MAX_RANKS ranks.
+ * Errors: a failure on one rank before the exchange (bad k_bits / sizes / pointers, a workspace
+ * too small, a device error in sampling, sample sort or partition) travels in a status word of the
+ * next all-gather, and EVERY rank returns the lowest rank's status together -- no rank is left
+ * waiting in a collective (RCCL has no timeout). Only a transport that cannot run at all (NULL
+ * transport or workspace, a workspace smaller than the collectives' control buffers) returns at
+ * once on that rank. Failures in or after the exchange (the exchange itself, the local sort) are
+ * the failing rank's own. */
 RSORT_API size_t rsort_multi_workspace_size(int64_t n, int64_t capacity, int k_bits, int pairs, int world);
 /* Over an RCCL communicator (`nccl_comm` is an ncclComm_t; RCCL result codes are all checked,
  * RSORT_ERR_COMM on failure). */
@@ -304,7 +321,9 @@ RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, in
                               void *d_workspace, size_t workspace_bytes, void *stream);
 
 /* Largest message of one exchange round, in keys (default and maximum 2^28 = 1 GiB; >= 64).
- * Process-wide; returns the previous value. Tests set small values to force several rounds. */
+ * Messages are cut into equal pieces of a multiple of 64 keys rounded DOWN, so no message exceeds
+ * the limit even when it is not a multiple of 64. Process-wide; returns the previous value. Tests
+ * set small values to force several rounds. */
 RSORT_API int64_t rsort_set_exchange_piece(int64_t keys);
 
 /* The communication the multi-GPU sort needs, as a plug-in (RCCL is one implementation, the

@@ -23,7 +23,7 @@ def run_bench(*args):
 
 def test_bench_headline_contract():
     d = run_bench("--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--cpu-n", str(1 << 20), "--cpu-reps", "1",
-                  "--cpu-rows", "18,24")
+                  "--cpu-rows", "18,24", "--configs-n", str((1 << 22) + 5), "--configs-reps", "5")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "vendor", "end_to_end"):
         assert k in d, k
@@ -38,17 +38,28 @@ def test_bench_headline_contract():
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     cb = d["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] == 1 and cb["value"] > 0
+    # what ran, from the library itself
+    assert d["config"]["lane_order_probe"] in (0, 1) and d["config"]["scatter_kernels"]
+    assert rf["kernel"].startswith("rs_scatter")
+    # the other BASELINE configurations, measured in the same run
+    assert set(d["configs"]) == {"c2", "zipf", "c4"}
+    for name, c in d["configs"].items():
+        assert c["verified"] is True and c["plan_check"] == 0, name
+        assert c["ms_per_sort"] > 0 and c["Mkeys_per_s"] > 0 and c["sorts"] == 5, name
+        assert 0 < c["scatter"]["frac"] < 1 and c["scatter"]["bytes_per_key"] == (16 if c["pairs"] else 8), name
+        assert c["scatter_kernels"], name
+    assert d["configs"]["c4"]["pairs"] and d["configs"]["c2"]["k_bits"] == 4
 
 
 def test_bench_group_chunks_reported():
-    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 27), "--no-cpu")
+    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 27), "--no-cpu", "--configs", "")
     assert d["config"]["group_chunk_passes"] in ([1, 3], [])  # [] on a device with other than 256 chunks
-    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 27), "--no-cpu", "--no-group-chunks")
+    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 27), "--no-cpu", "--no-group-chunks", "--configs", "")
     assert d["config"]["group_chunk_passes"] == []
 
 
 def test_bench_primitives_and_dist_path():
-    d = run_bench("--primitives", "--steps", "2", "--warmup", "1", "--keys", str(1 << 24))
+    d = run_bench("--primitives", "--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--configs", "")
     for k in ("copy", "histogram", "scan", "scatter", "local_sort", "partition_8"):
         assert d["primitives"][k]["ms"] > 0, k
     for impl in ("c", "torch"):
@@ -58,5 +69,6 @@ def test_bench_primitives_and_dist_path():
 
 
 def test_bench_pairs_zipf_verified():
-    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 24), "--dist", "zipf", "--pairs", "--no-cpu")
+    d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 24), "--dist", "zipf", "--pairs", "--no-cpu",
+                  "--configs", "")
     assert d["verified"] is True and d["config"]["pairs"] is True

@@ -1,13 +1,15 @@
-"""Full BASELINE sizes (2^26 and 2^30 keys, 2^30 pairs) on the GPU, checked through
-size-independent properties: sortedness, equality with the vendor sort (rocPRIM; a sort's
-output is unique), an order-independent multiset fingerprint, and for pairs the exact
-gather identity keys_out[i] == keys_in[vals_out[i]] plus stability (vals increasing within
-runs of equal keys, vals being the input index)."""
+"""Full BASELINE sizes (2^26 and 2^30 keys, 2^30 pairs) on the GPU: bit-exact against the
+oracle (the Baseline1.cu:15-64 restatement, pinned to the reference build) at C2, C3 and C4, and
+through size-independent properties: sortedness, equality with the vendor sort (rocPRIM; a sort's
+output is unique), an order-independent multiset fingerprint, and for pairs the exact gather
+identity keys_out[i] == keys_in[vals_out[i]] plus stability (vals increasing within runs of equal
+keys, vals being the input index). Beyond the configs: one sort of 2^31 + 12345 keys (rsort.h
+promises n < 2^32; every position is carried in u32)."""
 import numpy as np
 import pytest
 
 from _rs import rs
-from _util import zipf_cdf_u32
+from _util import oracle_sort, oracle_sort_pairs, zipf_cdf_u32
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -46,6 +48,52 @@ def test_fullsize_uniform(n, k):
     assert is_sorted(out)
     assert fingerprint(out) == fingerprint(keys)
     del ref
+
+
+@pytest.mark.parametrize("n,k", [(1 << 26, 4), (1 << 30, 8)])
+def test_fullsize_vs_baseline1(n, k):
+    """C2 (2^26, k=4) and C3 (2^30, k=8) uniform keys, bit-exact against the oracle -- the
+    reference's own self-check (Parallel7.cu:747-767: sortByHost vs sortByDevice) at the config
+    sizes. The oracle runs on the host (~9 s at 2^30)."""
+    keys = rs.empty_u32(n)
+    rs.gen_uniform(keys, 0x5EED)
+    out = rs.empty_u32(n)
+    rs.sort_device(keys, out, k)
+    torch.cuda.synchronize()
+    expect = oracle_sort(rs.to_numpy_u32(keys), k)
+    assert np.array_equal(rs.to_numpy_u32(out), expect)
+
+
+def test_fullsize_pairs_zipf_vs_oracle():
+    """C4 (2^30 Zipf keys + index payloads, k=8), bit-exact against the oracle's stable pairs sort
+    (the Baseline1 loop carrying the payload)."""
+    n = 1 << 30
+    keys = rs.empty_u32(n)
+    rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32()), 0x5EED)
+    vals = rs.empty_u32(n)
+    rs.gen_iota(vals, 0)
+    ko, vo = rs.empty_u32(n), rs.empty_u32(n)
+    rs.sort_device(keys, ko, 8, vals_in=vals, vals_out=vo)
+    torch.cuda.synchronize()
+    rk, rv = oracle_sort_pairs(rs.to_numpy_u32(keys), rs.to_numpy_u32(vals), 8)
+    assert np.array_equal(rs.to_numpy_u32(ko), rk)
+    assert np.array_equal(rs.to_numpy_u32(vo), rv)
+
+
+def test_beyond_2_31_keys():
+    """n = 2^31 + 12345 (8.6 GB per buffer), k = 8: every chunk, group and table position above
+    2^31 in u32. Checked on the device: sorted, the input's multiset fingerprint, equal to rocPRIM."""
+    n = (1 << 31) + 12345
+    keys = rs.empty_u32(n)
+    rs.gen_uniform(keys, 0xB16)
+    out = rs.empty_u32(n)
+    rs.sort_device(keys, out, 8)
+    fp_in = rs.fingerprint(keys)[0]
+    assert rs.fingerprint(out) == (fp_in, 0)
+    ref = rs.empty_u32(n)
+    rs.vendor_sort_device(keys, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
 
 
 def test_fullsize_pairs_zipf():

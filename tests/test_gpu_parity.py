@@ -352,6 +352,64 @@ def test_partition_stable(nb):
     assert np.array_equal(host(starts), exp)
 
 
+def _cus():
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+@pytest.mark.parametrize("nb,repeat", [(2, False), (8, True), (15, True), (16, False)])
+def test_partition_stable_large(nb, repeat):
+    """keys-only partitions of n >= 2 x CUs x 8192 keys run the 512 x 16 line tiles with
+    splitter digits (rsort_capi.cpp choose_geom). n = 2 x CUs x 8192 + odd, Zipf keys; with
+    `repeat`, splitters in the equal-key-bucket shape of the multi-GPU sort (v, v + 1 pairs, v + 1
+    equal to the next v, so some buckets are empty). Against numpy's stable argsort and the bucket
+    starts."""
+    n = 2 * _cus() * 8192 + 4099
+    x = zipf_keys(n, seed=nb + 100)
+    q = np.unique(x[:: max(1, n // 64)])
+    rng = np.random.default_rng(nb)
+    if repeat:
+        vs = [int(v) for v in np.sort(rng.choice(q, size=nb // 2, replace=False))]
+        vs[1] = vs[0] + 1  # splitters v0, v0 + 1, v0 + 1, v0 + 2: a repeated splitter, an empty bucket
+        split = np.array(sorted(sum(([v, v + 1] for v in vs), []))[: nb - 1], np.uint64)
+    else:
+        split = np.sort(rng.choice(q, size=nb - 1, replace=False)).astype(np.uint64)
+    split = np.minimum(split, 0xFFFFFFFF).astype(np.uint32)
+    assert split.size == nb - 1 and np.all(split[1:] >= split[:-1])
+    bucket = np.searchsorted(split, x, side="right")
+    order = np.argsort(bucket, kind="stable")
+    ko = rs.empty_u32(n)
+    starts = rs.empty_u32(nb + 1)
+    rs.partition_device(dev(x), ko, split.tolist(), starts)
+    torch.cuda.synchronize()
+    assert np.array_equal(host(ko), x[order])
+    exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
+    assert np.array_equal(host(starts), exp)
+
+
+def test_plan_check_and_kernels_used():
+    """rsort_plan_check reports the tail scans' self-check (0 = every next-pass table summed to n)
+    after k = 3, 4 sorts; rsort_scatter_kernels_used names what the dispatch launched."""
+    rs.scatter_kernels_used(reset=True)
+    for n, k in [((1 << 22) + 77, 4), ((1 << 21) - 3, 3)]:
+        x = uniform_keys(n, seed=n)
+        p = rs.plan(n, k)
+        ws = rs.workspace(p.workspace_bytes)
+        out = rs.empty_u32(n)
+        rs.sort_device(dev(x), out, k, ws=ws, plan_=p)
+        assert rs.plan_check(p, ws) == 0
+        assert np.array_equal(host(out), oracle_sort(x, k))
+    used = rs.scatter_kernels_used(reset=True)
+    assert used and all(u.startswith("rs_scatter") for u in used), used
+    assert any(u.startswith("rs_scatter_lines<4,") for u in used), used
+    n = 1 << 24
+    x = uniform_keys(n, seed=5)
+    out = rs.empty_u32(n)
+    rs.sort_device(dev(x), out, 8)
+    torch.cuda.synchronize()
+    used = rs.scatter_kernels_used()
+    assert any(u.startswith("rs_scatter_lines<8, 1024, 16, 32, false") for u in used), used
+
+
 # ------------------------------------------------------------------ reference harness (CLI)
 @pytest.mark.parametrize("args", [["--debug"], [], ["512", "4"], ["256", "5", "--n", "1000003"]])
 def test_reference_harness_cli(args):

@@ -160,3 +160,19 @@ def test_dist_sort_capacity_error_on_every_rank(tmp_path):
     world = 3
     mp.spawn(_cap_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert [(tmp_path / f"r{r}").read_text() for r in range(world)] == ["9"] * world
+
+
+def test_exchange_rounds_never_exceed_the_limit():
+    """pieces are a multiple of 64 keys rounded DOWN, so no message exceeds the limit
+    even when the limit is not a multiple of 64 (limit 65, max_message 130: pieces of 64, 3
+    rounds -- rounding up gave 128)."""
+    import multi
+    assert multi.exchange_rounds(130, 65) == (3, 64)
+    assert multi.exchange_rounds(0, 1 << 28) == (0, 0)
+    rng = np.random.default_rng(7)
+    for _ in range(2000):
+        m = int(rng.integers(1, 1 << 40))
+        limit = int(rng.integers(64, 1 << 30))
+        rounds, piece = multi.exchange_rounds(m, limit)
+        assert 64 <= piece <= limit and piece % 64 == 0
+        assert rounds * piece >= m > (rounds - 1) * piece
