@@ -37,6 +37,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -1655,6 +1656,303 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------ scatter (pairs, 128-B lines)
+// rs_scatter_pairs: the pass of rs_scatter_lines for key + value pairs with whole 128-B lines in BOTH
+// output arrays (G = 32 keys). rs_scatter_lines' layout cannot do that for pairs: its LDS lines map
+// one to one to global lines (every digit's segment starts on a line, T + 31R slots per array) and
+// the carries live in an LDS area of their own (32R slots per array): 2 x (T + 63R) x 4 B = 190 KB at
+// 8192-pair tiles, so pairs wrote 64-B lines (whose HBM floor is 1.3x that of 128-B lines,
+// dev/runlen_lab.hip: 3.74 vs 2.90 ms per 2^30 pairs). Here:
+//   * a digit's segment starts on a 16-B quad (not a line), so it wastes <= 3 slots, and it holds
+//     carry + this tile's keys INCLUDING the tail past the last whole line: <= T + 34R slots per array;
+//   * the tail goes back to REGISTERS (the digit's TPD threads hold 32 / TPD carry slots of keys
+//     and values each) and is written into the next tile's segment head in step 2: no carry area;
+//   * the output phase walks whole lines in order; a line's digit is the last digit whose first line
+//     is at or before it (one bit per line start in a bitmap + the digit at each start), its LDS and
+//     global positions the digit's record {global, LDS} + 32 x line.
+// 2 x (8192 + 34 x 256 + 36) x 4 B = 135 KB + counters + records: fits 160 KB beside 8192-pair tiles.
+// Per tile:
+//   1. per-wave digit histogram with returning adds = ranks (as rs_scatter_lines)
+//   2. segments (quad-aligned, packed with the whole-line count into one block scan), per-(wave,
+//      digit) LDS bases, the carry written from registers into the segment head, line marks
+//   3. stage keys and values at base + rank (tails included, no limit test)
+//   4. whole lines out (8 lanes x 16 B per array per line), the tails read back into registers
+// A chunk starts with `inv` invalid leading slots per digit (its first line begins before the
+// chunk's output) and ends with masked dword stores of the carries (both lines are shared with the
+// neighbouring chunks). Digit-group chunks (a.bounds) and the clustered-input ranking (CL) as in
+// rs_scatter_lines.
+template <int BITS, int THREADS, int KPT, int CL = 0>
+__global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int W = THREADS / kWave;
+    constexpr int SEG = kWave * KPT;
+    constexpr uint32_t T = THREADS * KPT;
+    constexpr uint32_t G = 32;                       // keys per 128-B line
+    constexpr uint32_t QPL = G / 4;                  // 16-B quads per line
+    constexpr uint32_t TPD = THREADS / R;            // threads per digit
+    constexpr uint32_t CPT = G / TPD;                // carry slots held per group thread
+    constexpr uint32_t CAP = T + (G - 1) * R + 3 * R;  // staged slots, worst case
+    constexpr uint32_t NLM = (T + (G - 1) * R) / G;    // whole lines per tile, worst case
+    constexpr uint32_t NBW = (NLM + 31) / 32;          // bitmap words
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    static_assert(R <= THREADS && TPD <= kWave && CPT % 4 == 0, "a digit's group in one wave, whole carry quads");
+    static_assert(CAP + 40 < 65536u && NLM < 65536u, "slot and line indices packed in 16 bits");
+
+    // [0, CAP) segments; [CAP, CAP + 32) the last tail read's overrun; CAP + 32 the padding sink
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[CAP + 36];
+    __shared__ __attribute__((aligned(16))) uint32_t s_v[CAP + 36];
+    constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
+    __shared__ uint32_t s_cnt[W * RS + 1];
+    __shared__ uint4 s_rec[R];        // per digit: {global - 32 x first line, LDS - 32 x first line, first line << 8 | inv}
+    __shared__ uint8_t s_mark[NLM + 1];  // digit of the line that starts a digit's lines
+    __shared__ uint32_t s_bits[NBW];     // line starts
+    __shared__ uint2 s_lrec[NLM];        // per whole line: {global key index, LDS index | inv << 16}
+    __shared__ uint32_t s_ws[W];
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = t / kWave;
+    const uint32_t lane = lane_id();
+    const uint32_t c = blockIdx.x;
+    const Digit<BITS, kDigitShift> dig{a.shift, 0, nullptr};
+    uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    uint32_t head = 0;
+    if (a.cl_select != nullptr && ((*a.cl_select != kGroupsWhole) != (CL != 0))) return;
+    if (a.bounds != nullptr && a.bounds[0] != 0u) {
+        const uint64_t b = a.bounds[1 + c];
+        cend = a.bounds[2 + c];
+        cbeg = b < cend ? (b & ~(uint64_t)(kWave - 1)) : cend;
+        head = (uint32_t)(b < cend ? b - cbeg : 0);
+    }
+
+    const uint32_t d_own = t / TPD;
+    const uint32_t sub = t % TPD;
+    const bool leader = sub == 0;
+    // group state (the same in every thread of the group): running global position, carry length,
+    // invalid leading slots of the chunk's first line; carry slots sub * CPT .. + CPT - 1 in ck / cv
+    uint32_t g_run, carry, inv;
+    {
+        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
+        carry = g & (G - 1u);
+        inv = carry;
+        g_run = g;
+    }
+    uint32_t ck[CPT], cv[CPT];
+#pragma unroll
+    for (uint32_t i = 0; i < CPT; ++i) ck[i] = cv[i] = 0u;
+
+    const uint32_t base = w * SEG + lane;
+    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[KPT]) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        uint32_t lb = base;
+        asm volatile("" : "+v"(lb));
+        const uint32_t *__restrict__ tk = a.kin + tb + lb;
+        const uint32_t *__restrict__ tv = a.vin + tb + lb;
+        if (valid == T) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                k[j] = tk[j * kWave];
+                v[j] = tv[j * kWave];
+            }
+        } else {
+            const uint32_t lim = valid > lb ? valid - lb : 0u;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool in = (uint32_t)(j * kWave) < lim;
+                k[j] = in ? tk[j * kWave] : 0u;
+                v[j] = in ? tv[j * kWave] : 0u;
+            }
+        }
+    };
+
+    // the digit of whole line V: the last marked line start at or before V
+    auto line_digit = [&](uint32_t V) {
+        uint32_t wi = V >> 5;
+        uint32_t m = s_bits[wi] & (0xFFFFFFFFu >> (31u - (V & 31u)));
+        while (m == 0u) m = s_bits[--wi];  // (line 0 is always marked)
+        return (uint32_t)s_mark[wi * 32u + 31u - (uint32_t)__builtin_clz(m)];
+    };
+    auto store_item = [&](uint32_t item) {
+        const uint32_t V = item / QPL, q = (item % QPL) * 4u;
+        const uint2 lr = s_lrec[V];
+        const uint32_t li = (lr.y & 0xFFFFu) + q;
+        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_k[li]);
+        const u32x4 vv = *reinterpret_cast<const u32x4 *>(&s_v[li]);
+        const uint64_t gp = (uint64_t)(lr.x + q);
+        const uint32_t lo = lr.y >> 16;
+        if (lo <= q) {
+            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
+            __builtin_nontemporal_store(vv, reinterpret_cast<u32x4 *>(a.vout + gp));
+        } else {
+            // the chunk's first line of this digit: lanes below lo belong to the previous chunk
+#pragma unroll
+            for (uint32_t x = 0; x < 4; ++x)
+                if (lo <= q + x) {
+                    a.kout[gp + x] = kv[x];
+                    a.vout[gp + x] = vv[x];
+                }
+        }
+    };
+
+    uint32_t key[KPT], val[KPT];
+    if (cbeg < cend) load_tile(cbeg, key, val);
+    uint32_t hotd = 0xFFFFFFFFu;
+
+    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const bool full = valid == T && head == 0;
+        const uint64_t nb = tb + T;
+        uint32_t plim = valid > base ? valid - base : 0u;
+        asm volatile("" : "+v"(plim));
+        const bool h0 = base >= head;
+        head = 0;
+        // ---- 1. per-wave digit histogram; the returning add is the key's rank among its wave's
+        //      keys of that digit (lane order, kRankAtomic); two ranks per register
+#pragma unroll
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
+        uint32_t rk[(KPT + 1) / 2];
+        uint32_t nkey[KPT], nval[KPT];
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t dj = dig(key[j]);
+                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = dig(key[j]);
+                uint32_t r = 0;
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            }
+        }
+        if (nb < cend) load_tile(nb, nkey, nval);
+        // (the previous tile's step 4 has read the bitmap: behind the barrier below)
+        __syncthreads();
+
+        // ---- 2. segments, bases, carry in, line marks
+        constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
+        uint32_t part = 0;
+        uint32_t wx[WPT];
+        if (sub < (uint32_t)W) {
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
+                part += wx[i];
+            }
+        }
+        uint32_t gpre, cnt;
+        group_scan<TPD>(part, sub, gpre, cnt);
+        // (carry, g_run, inv are the same in every thread of the group)
+        const uint32_t A = g_run - carry;          // line-aligned
+        const uint32_t pending = carry + cnt;      // slots from A on
+        const uint32_t wl = pending / G;           // whole lines written this tile
+        const uint32_t seg = (pending + 3u) & ~3u;
+        if (t < NBW) s_bits[t] = 0u;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
+        const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
+        const uint32_t nlines = tot >> 16;
+        if (sub < (uint32_t)W) {
+            uint32_t acc = S + carry + gpre;
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                if (v < (uint32_t)W) s_cnt[v * RS + d_own] = acc;
+                acc += wx[i];
+            }
+        }
+        // the carry from registers into the segment head, whole quads (a quad past the carry's end
+        // lies inside the segment and is overwritten by step 3)
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; i += 4) {
+            if (sub * CPT + i < carry) {
+                *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
+                *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+            }
+        }
+        if (leader) {
+            s_rec[d_own] = make_uint4(A - LS * G, S - LS * G, (LS << 8) | inv, 0u);
+            if (wl > 0) {
+                s_mark[LS] = (uint8_t)d_own;
+                atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
+            }
+        }
+        __syncthreads();
+
+        // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
+        //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
+        //      (batches of 8: all reads before the stores)
+        for (uint32_t V = t; V < nlines; V += THREADS) {
+            const uint4 rec = s_rec[line_digit(V)];
+            const uint32_t lo = (rec.z >> 8) == V ? (rec.z & 0xFFu) : 0u;
+            s_lrec[V] = make_uint2(rec.x + V * G, (rec.y + V * G) | (lo << 16));
+        }
+        constexpr int SB = KPT < 8 ? KPT : 8;
+        static_assert(KPT % SB == 0, "whole batches of slots");
+#pragma unroll
+        for (int j0 = 0; j0 < KPT; j0 += SB) {
+            uint32_t pp[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                asm volatile("" : "+v"(key[j]));
+                pp[u] = s_cnt[w * RS + dig(key[j])] + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                uint32_t idx = pp[u];
+                if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
+                s_k[idx] = key[j];
+                s_v[idx] = val[j];
+            }
+        }
+        __syncthreads();
+
+        // ---- 4. the tails back into the carry registers; whole lines out
+        {
+            const uint32_t tl0 = S + wl * G + sub * CPT;  // quad-aligned
+#pragma unroll
+            for (uint32_t i = 0; i < CPT; i += 4) {
+                const u32x4 kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+                const u32x4 vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
+                ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
+                cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
+            }
+        }
+        const uint32_t nq = nlines * QPL;
+        for (uint32_t item = t; item < nq; item += 2 * THREADS) {
+            store_item(item);
+            if (item + THREADS < nq) store_item(item + THREADS);
+        }
+        if (wl > 0) inv = 0;
+        carry = pending - wl * G;
+        g_run += cnt;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            key[j] = nkey[j];
+            val[j] = nval[j];
+        }
+    }
+    // ---- chunk end: the carries (slots inv .. carry - 1 from the line at g_run - carry)
+    if (cbeg < cend) {
+        const uint64_t A = (uint64_t)(g_run - carry);
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; ++i) {
+            const uint32_t x = sub * CPT + i;
+            if (x >= inv && x < carry) {
+                a.kout[A + x] = ck[i];
+                a.vout[A + x] = cv[i];
+            }
+        }
+    }
+}
+
 // Top-bits histogram of every stride-th 256-key block (the multi-GPU sort's splitter sample):
 // 1024 threads take four sampled blocks per iteration into 2^top_bits LDS counters, then add
 // them into the zeroed hist (one workgroup per CU keeps that final add to 2^top_bits per CU).
@@ -1795,6 +2093,29 @@ static void *reg_lines() {
     return fn;
 }
 
+template <int BITS, int THREADS, int KPT, int CL = 0>
+static void *reg_pairs() {
+    void *fn = reinterpret_cast<void *>(&rs_scatter_pairs<BITS, THREADS, KPT, CL>);
+    static const bool once = [fn] {
+        char nm[96];
+        snprintf(nm, sizeof nm, "rs_scatter_pairs<%d, %d, %d, %d>", BITS, THREADS, KPT, CL);
+        register_kernel(fn, nm);
+        return true;
+    }();
+    (void)once;
+    return fn;
+}
+
+// Pairs with k = 6..8 write 128-B lines through rs_scatter_pairs; RSORT_PAIRS64=1 in the environment
+// selects rs_scatter_lines' 64-B-line pairs kernel instead (A/B measurements, dev/lab.sh).
+static bool pairs_lines64() {
+    static const bool v = [] {
+        const char *e = getenv("RSORT_PAIRS64");
+        return e != nullptr && e[0] != '\0' && e[0] != '0';
+    }();
+    return v;
+}
+
 template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW>
 static void *reg_scatter() {
     void *fn = reinterpret_cast<void *>(&rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, DMODE, MINW>);
@@ -1897,6 +2218,10 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         // only (dev/scatter_lab LAB_PAIRS, 2^30: 4.24 -> 3.96 ms; nt loads 4.66 ms)
         constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
         if (geom == GL) {
+            if constexpr (PAIRS && BITS >= 6) {
+                if (rank == kRankAtomic && aligned16 && !pairs_lines64())
+                    return reg_pairs<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt>();
+            }
             if (rank == kRankAtomic && aligned16)
                 return reg_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
                                                                   PAIRS ? kLineKeysPairs : kLineKeys, PAIRS,
@@ -2080,6 +2405,8 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
             cl = reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
         else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2>))
             cl = reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_pairs<8, 512, 16>))
+            cl = reg_pairs<8, 512, 16, 1>();
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
