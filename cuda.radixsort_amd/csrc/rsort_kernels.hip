@@ -1656,6 +1656,27 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     }
 }
 
+// Lab builds (-DRSORT_STAMPS, dev/pairs_lab.hip): per-phase s_memtime cycle totals of thread 0 into
+// ScatterArgs::stamps[workgroup * 8 + phase]. Empty in the library.
+#ifdef RSORT_STAMPS
+#define RS_STAMP_DECL unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev_ = __builtin_amdgcn_s_memtime();
+#define RS_STAMP(i)                                                   \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        st_acc_[i] += now_ - st_prev_;                                \
+        st_prev_ = now_;                                              \
+    } while (0)
+#define RS_STAMP_FLUSH()                                                                   \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && a.stamps)                                                  \
+            for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 8 + i_] = st_acc_[i_];    \
+    } while (0)
+#else
+#define RS_STAMP_DECL
+#define RS_STAMP(i)
+#define RS_STAMP_FLUSH()
+#endif
+
 // ------------------------------------------------------------------------------ scatter (pairs, 128-B lines)
 // rs_scatter_pairs: the pass of rs_scatter_lines for key + value pairs with whole 128-B lines in BOTH
 // output arrays (G = 32 keys). rs_scatter_lines' layout cannot do that for pairs: its LDS lines map
@@ -1681,7 +1702,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 // chunk's output) and ends with masked dword stores of the carries (both lines are shared with the
 // neighbouring chunks). Digit-group chunks (a.bounds) and the clustered-input ranking (CL) as in
 // rs_scatter_lines.
-template <int BITS, int THREADS, int KPT, int CL = 0>
+template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1>
 __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -1794,149 +1815,178 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
         }
     };
 
-    uint32_t key[KPT], val[KPT];
-    if (cbeg < cend) load_tile(cbeg, key, val);
+    // The tile step. PF = 1: the next tile's loads go into nkey at the end of the rank phase and
+    // move into key at the end of the step. PF = 2: two register sets alternate (the loop is unrolled
+    // by two); a tile's set takes the loads of the tile two ahead as soon as it is staged.
     uint32_t hotd = 0xFFFFFFFFu;
+    RS_STAMP_DECL
+    auto tile_step = [&](const uint64_t tb, uint32_t (&key)[KPT], uint32_t (&val)[KPT]) {
+            const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+            const bool full = valid == T && head == 0;
+            const uint64_t nb = tb + T;
+            uint32_t plim = valid > base ? valid - base : 0u;
+            asm volatile("" : "+v"(plim));
+            const bool h0 = base >= head;
+            head = 0;
+            // ---- 1. per-wave digit histogram; the returning add is the key's rank among its wave's
+            //      keys of that digit (lane order, kRankAtomic); two ranks per register
+    #pragma unroll
+            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
+            uint32_t rk[(KPT + 1) / 2];
+            uint32_t nkey[PF == 1 ? KPT : 1], nval[PF == 1 ? KPT : 1];
+            if (full) {
+    #pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t dj = dig(key[j]);
+                    const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            } else {
+    #pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t d = dig(key[j]);
+                    uint32_t r = 0;
+                    if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            }
+            if constexpr (PF == 1) {
+                if (nb < cend) load_tile(nb, nkey, nval);
+            }
+            // (the previous tile's step 4 has read the bitmap: behind the barrier below)
+            __syncthreads();
+            RS_STAMP(0);
 
-    for (uint64_t tb = cbeg; tb < cend; tb += T) {
-        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        const bool full = valid == T && head == 0;
-        const uint64_t nb = tb + T;
-        uint32_t plim = valid > base ? valid - base : 0u;
-        asm volatile("" : "+v"(plim));
-        const bool h0 = base >= head;
-        head = 0;
-        // ---- 1. per-wave digit histogram; the returning add is the key's rank among its wave's
-        //      keys of that digit (lane order, kRankAtomic); two ranks per register
-#pragma unroll
-        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
-        uint32_t rk[(KPT + 1) / 2];
-        uint32_t nkey[KPT], nval[KPT];
-        if (full) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t dj = dig(key[j]);
-                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
-                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            // ---- 2. segments, bases, carry in, line marks
+            constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
+            uint32_t part = 0;
+            uint32_t wx[WPT];
+            if (sub < (uint32_t)W) {
+    #pragma unroll
+                for (uint32_t i = 0; i < WPT; ++i) {
+                    const uint32_t v = sub * WPT + i;
+                    wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
+                    part += wx[i];
+                }
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t d = dig(key[j]);
-                uint32_t r = 0;
-                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
-                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            uint32_t gpre, cnt;
+            group_scan<TPD>(part, sub, gpre, cnt);
+            // (carry, g_run, inv are the same in every thread of the group)
+            const uint32_t A = g_run - carry;          // line-aligned
+            const uint32_t pending = carry + cnt;      // slots from A on
+            const uint32_t wl = pending / G;           // whole lines written this tile
+            const uint32_t seg = (pending + 3u) & ~3u;
+            if (t < NBW) s_bits[t] = 0u;
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
+            const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
+            const uint32_t nlines = tot >> 16;
+            if (sub < (uint32_t)W) {
+                uint32_t acc = S + carry + gpre;
+    #pragma unroll
+                for (uint32_t i = 0; i < WPT; ++i) {
+                    const uint32_t v = sub * WPT + i;
+                    if (v < (uint32_t)W) s_cnt[v * RS + d_own] = acc;
+                    acc += wx[i];
+                }
             }
-        }
-        if (nb < cend) load_tile(nb, nkey, nval);
-        // (the previous tile's step 4 has read the bitmap: behind the barrier below)
-        __syncthreads();
-
-        // ---- 2. segments, bases, carry in, line marks
-        constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
-        uint32_t part = 0;
-        uint32_t wx[WPT];
-        if (sub < (uint32_t)W) {
-#pragma unroll
-            for (uint32_t i = 0; i < WPT; ++i) {
-                const uint32_t v = sub * WPT + i;
-                wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
-                part += wx[i];
-            }
-        }
-        uint32_t gpre, cnt;
-        group_scan<TPD>(part, sub, gpre, cnt);
-        // (carry, g_run, inv are the same in every thread of the group)
-        const uint32_t A = g_run - carry;          // line-aligned
-        const uint32_t pending = carry + cnt;      // slots from A on
-        const uint32_t wl = pending / G;           // whole lines written this tile
-        const uint32_t seg = (pending + 3u) & ~3u;
-        if (t < NBW) s_bits[t] = 0u;
-        uint32_t tot;
-        const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
-        const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
-        const uint32_t nlines = tot >> 16;
-        if (sub < (uint32_t)W) {
-            uint32_t acc = S + carry + gpre;
-#pragma unroll
-            for (uint32_t i = 0; i < WPT; ++i) {
-                const uint32_t v = sub * WPT + i;
-                if (v < (uint32_t)W) s_cnt[v * RS + d_own] = acc;
-                acc += wx[i];
-            }
-        }
-        // the carry from registers into the segment head, whole quads (a quad past the carry's end
-        // lies inside the segment and is overwritten by step 3)
-#pragma unroll
-        for (uint32_t i = 0; i < CPT; i += 4) {
-            if (sub * CPT + i < carry) {
-                *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
-                *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
-            }
-        }
-        if (leader) {
-            s_rec[d_own] = make_uint4(A - LS * G, S - LS * G, (LS << 8) | inv, 0u);
-            if (wl > 0) {
-                s_mark[LS] = (uint8_t)d_own;
-                atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
-            }
-        }
-        __syncthreads();
-
-        // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
-        //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
-        //      (batches of 8: all reads before the stores)
-        for (uint32_t V = t; V < nlines; V += THREADS) {
-            const uint4 rec = s_rec[line_digit(V)];
-            const uint32_t lo = (rec.z >> 8) == V ? (rec.z & 0xFFu) : 0u;
-            s_lrec[V] = make_uint2(rec.x + V * G, (rec.y + V * G) | (lo << 16));
-        }
-        constexpr int SB = KPT < 8 ? KPT : 8;
-        static_assert(KPT % SB == 0, "whole batches of slots");
-#pragma unroll
-        for (int j0 = 0; j0 < KPT; j0 += SB) {
-            uint32_t pp[SB];
-#pragma unroll
-            for (int u = 0; u < SB; ++u) {
-                const int j = j0 + u;
-                asm volatile("" : "+v"(key[j]));
-                pp[u] = s_cnt[w * RS + dig(key[j])] + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < SB; ++u) {
-                const int j = j0 + u;
-                uint32_t idx = pp[u];
-                if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
-                s_k[idx] = key[j];
-                s_v[idx] = val[j];
-            }
-        }
-        __syncthreads();
-
-        // ---- 4. the tails back into the carry registers; whole lines out
-        {
-            const uint32_t tl0 = S + wl * G + sub * CPT;  // quad-aligned
-#pragma unroll
+            // the carry from registers into the segment head, whole quads (a quad past the carry's end
+            // lies inside the segment and is overwritten by step 3)
+    #pragma unroll
             for (uint32_t i = 0; i < CPT; i += 4) {
-                const u32x4 kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
-                const u32x4 vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
-                ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
-                cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
+                if (sub * CPT + i < carry) {
+                    *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
+                    *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+                }
             }
-        }
-        const uint32_t nq = nlines * QPL;
-        for (uint32_t item = t; item < nq; item += 2 * THREADS) {
-            store_item(item);
-            if (item + THREADS < nq) store_item(item + THREADS);
-        }
-        if (wl > 0) inv = 0;
-        carry = pending - wl * G;
-        g_run += cnt;
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            key[j] = nkey[j];
-            val[j] = nval[j];
+            if (leader) {
+                s_rec[d_own] = make_uint4(A - LS * G, S - LS * G, (LS << 8) | inv, 0u);
+                if (wl > 0) {
+                    s_mark[LS] = (uint8_t)d_own;
+                    atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
+                }
+            }
+            __syncthreads();
+            RS_STAMP(1);
+
+            // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
+            //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
+            //      (batches of 8: all reads before the stores)
+            for (uint32_t V = t; V < nlines; V += THREADS) {
+                const uint4 rec = s_rec[line_digit(V)];
+                const uint32_t lo = (rec.z >> 8) == V ? (rec.z & 0xFFu) : 0u;
+                s_lrec[V] = make_uint2(rec.x + V * G, (rec.y + V * G) | (lo << 16));
+            }
+            RS_STAMP(2);
+            constexpr int SB = KPT < 8 ? KPT : 8;
+            static_assert(KPT % SB == 0, "whole batches of slots");
+    #pragma unroll
+            for (int j0 = 0; j0 < KPT; j0 += SB) {
+                uint32_t pp[SB];
+    #pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u;
+                    asm volatile("" : "+v"(key[j]));
+                    pp[u] = s_cnt[w * RS + dig(key[j])] + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                for (int u = 0; u < SB; ++u) {
+                    const int j = j0 + u;
+                    uint32_t idx = pp[u];
+                    if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
+                    s_k[idx] = key[j];
+                    s_v[idx] = val[j];
+                }
+            }
+            // PF = 2: this tile's registers are free (staged): the tile after next goes into them, in
+            // flight through this tile's output and the whole next tile
+            if constexpr (PF == 2) {
+                if (nb + T < cend) load_tile(nb + T, key, val);
+            }
+            __syncthreads();
+            RS_STAMP(3);
+
+            // ---- 4. the tails back into the carry registers (the quads holding any); whole lines out
+            {
+                const uint32_t tl0 = S + wl * G + sub * CPT;  // quad-aligned
+                const uint32_t ncarry = pending - wl * G;
+    #pragma unroll
+                for (uint32_t i = 0; i < CPT; i += 4) {
+                    if (sub * CPT + i >= ncarry) break;
+                    const u32x4 kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+                    const u32x4 vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
+                    ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
+                    cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
+                }
+            }
+            const uint32_t nq = nlines * QPL;
+            for (uint32_t item = t; item < nq; item += 2 * THREADS) {
+                store_item(item);
+                if (item + THREADS < nq) store_item(item + THREADS);
+            }
+            RS_STAMP(4);
+            if (wl > 0) inv = 0;
+            carry = pending - wl * G;
+            g_run += cnt;
+            if constexpr (PF == 1) {
+    #pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    key[j] = nkey[j];
+                    val[j] = nval[j];
+                }
+            }
+    };
+    uint32_t keyA[KPT], valA[KPT];
+    if (cbeg < cend) load_tile(cbeg, keyA, valA);
+    if constexpr (PF == 1) {
+        for (uint64_t tb = cbeg; tb < cend; tb += T) tile_step(tb, keyA, valA);
+    } else {
+        uint32_t keyB[KPT], valB[KPT];
+        if (cbeg + T < cend) load_tile(cbeg + T, keyB, valB);
+        for (uint64_t tb = cbeg; tb < cend; tb += 2 * T) {
+            tile_step(tb, keyA, valA);
+            if (tb + T < cend) tile_step(tb + T, keyB, valB);
         }
     }
     // ---- chunk end: the carries (slots inv .. carry - 1 from the line at g_run - carry)
@@ -1951,6 +2001,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             }
         }
     }
+    RS_STAMP_FLUSH();
 }
 
 // Top-bits histogram of every stride-th 256-key block (the multi-GPU sort's splitter sample):

@@ -1,3 +1,4 @@
+# Backs DESIGN §5 step 6: this RCCL leaves the second half of a >= 2 GiB message unwritten (1 GiB arrives whole).
 """dev/a2a_lab.py -- does all_to_all_single (RCCL, world 1) copy large int32 messages?"""
 import os
 

@@ -1,3 +1,4 @@
+// Backs DESIGN §8 "Histograms": two concurrent readers of one chunk cost two reads (request-rate bound).
 // dualread_lab.hip -- development harness: can two workgroups count the same chunk of keys for the
 // price of one HBM read? 256 chunks of n/256 keys; each workgroup (1024 threads, one per CU: 128 KB
 // of LDS) reads its chunk with non-temporal 16-B loads and adds one LDS atomic per key (a

@@ -1,3 +1,4 @@
+# Backs DESIGN §8 "Launch gaps": a sort replayed as a HIP graph is no faster than direct launches.
 """dev/graph_lab.py -- launch-gap cost: the same device sort timed as direct launches and as a
 replayed HIP graph (torch.cuda.CUDAGraph capture of rsort_sort_planned), C2 and C3 shapes."""
 import os, sys, time

@@ -1,3 +1,4 @@
+// Backs DESIGN §8 "Histograms": two 8-bit joint tables in one key read are LDS-bound (0.95 ms uniform, 6.8 ms Zipf).
 // joint2_lab.hip -- development harness (not part of the library): can pass 0's key read count two
 // joint tables at once? Times, over 2^30 keys in 256 chunks (one 1024-thread workgroup each):
 //   A  the library's layout: (digit 0, digit 1) pairs in 16-bit LDS counters, spill at 2^15

@@ -1,13 +1,27 @@
 #!/bin/bash
 # dev/lab.sh -- the one lab runner for GPU sessions (gpurun): `bash dev/lab.sh <experiment> [args]`.
 # Every GPU step runs under its own timeout; the script stops at the first crash / timeout (a plain
-# test failure, pytest rc 1, does not stop it). Output goes to gpurun_out/<experiment>*.
+# test failure, pytest rc 1, does not stop it). Output goes to gpurun_out/. The dev/*_lab binaries
+# are built on the CPU side first (the command in each file's header); dev/README.md says which
+# DESIGN.md claim each lab backs.
 #
-#   round         pytest -m gpu (all) + the default bench line            (the round-end tiers)
-#   pairs         the pairs tests + the C4 config, new 128-B kernel and 64-B kernel (RSORT_PAIRS64=1)
-#   bench [args]  bench.py with extra args
-#   prof [args]   rocprofv3 --kernel-trace --stats of bench.py with extra args (profiles)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+#   round            pytest -m gpu (all) + the default bench line (what the driver runs at round end)
+#   tests [-k EXPR]  pytest -m gpu, optionally filtered
+#   pairs            the pairs tests + C4 and Zipf keys through bench.py, then C4 with the 64-B-line
+#                    pairs kernel (RSORT_PAIRS64=1) for A/B on the same box
+#   pairslab         dev/pairs_lab: one pairs pass, 64-B vs 128-B kernels, per-phase cycles
+#   lines            dev/lines_exp: the keys line-kernel variants, uniform passes 0/1, Zipf passes 0..3
+#   zcl              dev/lines_exp "pad": clustered-kernel rank variants, uniform pass 0, Zipf passes 1, 2
+#   bench [args]     bench.py with extra args (LAB_TAG names the output)
+#   kt TAG [args]    rocprofv3 per-launch kernel trace of a short bench run (gpurun_out/kt_TAG;
+#                    dev/ktall.py / dev/ktsum.py read it)
+#   variants V...    dev/var_V.so (dev/build_variant.sh) over the box's librsort.so in turn: kernel
+#                    traces of the C3, Zipf-keys and all-equal benches
+#   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
+#   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
+#   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R" || exit 1
 mkdir -p gpurun_out
 exp=$1
 shift
@@ -16,14 +30,26 @@ ok_or_stop() {  # pytest rc 0/1 continue, anything else (crash, timeout) stops t
     echo "[lab] $2 rc=$rc"
     if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then exit "$rc"; fi
 }
+stop_unless_ok() {
+    local rc=$1
+    echo "[lab] $2 rc=$rc"
+    [ "$rc" -eq 0 ] || exit "$rc"
+}
 run_bench() {  # name, args...
     local name=$1
     shift
     timeout -k 10 300 python bench.py "$@" > "gpurun_out/$name.json" 2> "gpurun_out/$name.err"
-    local rc=$?
-    echo "[lab] bench $name rc=$rc"
-    [ $rc -eq 0 ] || exit $rc
+    stop_unless_ok $? "bench $name"
     tail -c 2500 "gpurun_out/$name.json"
+}
+kt() {  # tag, bench args...
+    local tag=$1
+    shift
+    rm -rf "$R/gpurun_out/kt_$tag"
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/kt_$tag" -- \
+        python3 "$R/bench.py" --no-cpu --no-e2e --no-vendor --configs "" --steps 2 --warmup 1 "$@" \
+        > "$R/gpurun_out/kt_$tag.log" 2>&1)
+    stop_unless_ok $? "kt $tag"
 }
 case "$exp" in
 round)
@@ -32,6 +58,12 @@ round)
     ok_or_stop $? pytest
     tail -n 3 gpurun_out/round_tests.log
     run_bench round_bench --steps 20 --warmup 5
+    ;;
+tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail 8 --timeout 300 --timeout-method thread "$@" \
+        > gpurun_out/lab_tests.log 2>&1
+    ok_or_stop $? pytest
+    grep -E "passed|failed|FAILED|Error" gpurun_out/lab_tests.log | tail -n 20
     ;;
 pairs)
     timeout -k 10 600 python -u -m pytest tests -m gpu -v -k "pairs or clustered or cut_plan or group" \
@@ -42,17 +74,72 @@ pairs)
     RSORT_PAIRS64=1 run_bench pairs_64 --steps 5 --warmup 2 --keys 16777216 --no-cpu --no-vendor --no-e2e \
         --configs c4 "$@"
     ;;
+pairslab)
+    : > gpurun_out/pairslab.log
+    for cfg in "0 0" "1 0" "1 1"; do
+        set -- $cfg
+        PL_ZIPF=$1 PL_PASS=$2 timeout -k 10 120 dev/pairs_lab 30 >> gpurun_out/pairslab.log 2>&1
+        rc=$?
+        echo "[lab] pairs_lab zipf=$1 pass=$2 rc=$rc"
+        [ $rc -eq 0 ] || [ $rc -eq 3 ] || exit $rc
+    done
+    cat gpurun_out/pairslab.log
+    ;;
+lines)
+    : > gpurun_out/lab_lines.log
+    timeout -k 10 100 dev/lines_exp 30 "$@" >> gpurun_out/lab_lines.log 2>&1 || exit $?
+    LX_PASS=1 timeout -k 10 100 dev/lines_exp 30 "$@" >> gpurun_out/lab_lines.log 2>&1 || exit $?
+    for p in 0 1 2 3; do
+        LX_ZIPF=1 LX_PASS=$p timeout -k 10 100 dev/lines_exp 30 "$@" >> gpurun_out/lab_lines.log 2>&1 || exit $?
+    done
+    cat gpurun_out/lab_lines.log
+    ;;
+zcl)
+    : > gpurun_out/lab_zcl.log
+    timeout -k 10 100 dev/lines_exp 30 "pad" >> gpurun_out/lab_zcl.log 2>&1 || exit $?
+    for p in 1 2; do
+        LX_ZIPF=1 LX_PASS=$p timeout -k 10 100 dev/lines_exp 30 "pad" >> gpurun_out/lab_zcl.log 2>&1 || exit $?
+    done
+    cat gpurun_out/lab_zcl.log
+    ;;
 bench)
     run_bench "bench_${LAB_TAG:-x}" "$@"
     ;;
+kt)
+    kt "$@"
+    ;;
+variants)
+    for v in "$@"; do
+        cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so
+        kt "c3_$v"
+        kt "z_$v" --dist zipf
+        kt "e_$v" --dist equal
+    done
+    ;;
 prof)
-    export TMPDIR=/tmp
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${LAB_TAG:-x} -o run -- \
-        python bench.py "$@" > gpurun_out/prof_${LAB_TAG:-x}.log 2>&1
-    echo "[lab] prof rc=$?"
+    tag=$1
+    shift
+    bash profiles/run_profiles.sh "$tag" "$@"
+    stop_unless_ok $? "prof $tag"
+    ;;
+pmc)
+    C="TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum TCP_TCC_WRITE_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCC_BUSY_avr TCC_EA0_WRREQ_STALL_sum"
+    (cd /tmp && TMPDIR=/tmp timeout -s KILL 200 rocprofv3 --pmc $C -d "$R/gpurun_out/pmc_a" -o run -- \
+        "$R/dev/scatter_lab" 30 "k8 1024x16 lines16" > "$R/gpurun_out/pmc_a.log" 2>&1) || exit $?
+    (cd /tmp && TMPDIR=/tmp timeout -s KILL 200 rocprofv3 --pmc $C -d "$R/gpurun_out/pmc_b" -o run -- \
+        "$R/dev/wc_lab" 30 > "$R/gpurun_out/pmc_b.log" 2>&1) || exit $?
+    python3 dev/pmcdb.py gpurun_out/pmc_a gpurun_out/pmc_b
+    ;;
+dist)
+    rm -rf "$R/gpurun_out/prof_dist"
+    (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$R/gpurun_out/prof_dist" -- python3 "$R/bench.py" --no-cpu --no-e2e --configs "" --dist-path \
+        --steps 3 --warmup 1 "$@" > "$R/gpurun_out/prof_dist.log" 2>&1)
+    stop_unless_ok $? dist
+    tail -c 1500 "$R/gpurun_out/prof_dist.log"
     ;;
 *)
-    echo "unknown experiment: $exp"
+    echo "unknown experiment: $exp (see the header of dev/lab.sh)"
     exit 2
     ;;
 esac

@@ -1,3 +1,4 @@
+// Backs DESIGN §3 "Ranking": gfx950 serves same-address ds_add_rtn lanes in lane order (the kRankAtomic premise).
 // lds_order_lab.hip -- does a wave64 ds_add_rtn_u32 whose lanes hit the same LDS address
 // return values in ascending lane order (lane i gets old + #lower lanes with that address)?
 // If it always does, the per-wave digit rank of a key is one returning LDS atomic and the

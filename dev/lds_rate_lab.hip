@@ -1,3 +1,4 @@
+// Backs DESIGN §3 "Ranking": LDS cycles per wave instruction for the ranking access shapes (127 cycles when 64 lanes share a counter).
 // lds_rate_lab.hip -- development harness: LDS cost per wave-instruction for the access shapes
 // of the scatter kernel's ranking: random-digit ds_add_u32 / ds_add_rtn_u32 / ds_read_b32 /
 // ds_write_b32 / ds_read_b64 into per-wave 256-entry counter arrays, 1024-thread workgroups,

@@ -1,3 +1,4 @@
+// Backs DESIGN §3 "Clustered input" and per-pass notes: rs_scatter_lines knob variants (OUTB2, COPY64, pad rows, rank candidates), uniform and Zipf passes 0..3.
 // lines_exp.hip -- development harness (not part of the library): experimental copies of the
 // keys-only rs_scatter_lines pass (cuda.radixsort_amd/csrc/rsort_kernels.hip) with knobs, timed
 // against the library kernel on the same input and checked against its output.

@@ -1,0 +1,189 @@
+// Backs DESIGN §3 "Pairs": one k = 8 pairs pass, 64-B-line rs_scatter_lines vs 128-B-line rs_scatter_pairs, with per-phase cycles.
+// pairs_lab.hip -- development harness (not part of the library), backing DESIGN §3 "Pairs": one
+// k = 8 pairs pass (2^lg pairs, 8192-pair tiles, 256 fixed chunks) through the 64-B-line pairs kernel
+// (rs_scatter_lines<8, 512, 16, 16, true, ...>) and the 128-B-line one (rs_scatter_pairs), plain and
+// clustered-input (CL) ranking, timed with HIP events and checked equal; per-phase s_memtime cycles
+// per tile of rs_scatter_pairs (RS_STAMP, thread 0 of each workgroup).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc \
+//         dev/pairs_lab.hip -o dev/pairs_lab && dev/pairs_lab [lg=30]
+//   PL_ZIPF=1: Zipf(s=1) keys over 2^20 ranks (the C4 workload); PL_PASS=1: time pass 1 (digit 1) on
+//   pass 0's output (clustered for Zipf keys); PL_REPS=n.
+#define RSORT_LAB_LITE
+#define RSORT_STAMPS
+#include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+using namespace rsort;
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            printf("HIP error %s at line %d\n", hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+static int env_int(const char *n, int d) {
+    const char *e = getenv(n);
+    return e ? atoi(e) : d;
+}
+
+int main(int argc, char **argv) {
+    const int lg = argc > 1 ? atoi(argv[1]) : 30;
+    const uint64_t n = 1ull << lg;
+    const int zipf = env_int("PL_ZIPF", 0), pass = env_int("PL_PASS", 0), reps = env_int("PL_REPS", 5);
+    constexpr uint32_t R = 256, TILE = 8192, CH = 256;
+    const uint64_t tiles = (n + TILE - 1) / TILE, tpc = (tiles + CH - 1) / CH;
+    const uint64_t chunk_keys = tpc * TILE;
+    const uint32_t chunks = (uint32_t)((tiles + tpc - 1) / tpc);
+    uint32_t *k0, *v0, *ka, *va, *kb, *vb, *table, *bsums, *cdf;
+    unsigned long long *stamps;
+    CK(hipMalloc(&k0, n * 4));
+    CK(hipMalloc(&v0, n * 4));
+    CK(hipMalloc(&ka, n * 4));
+    CK(hipMalloc(&va, n * 4));
+    CK(hipMalloc(&kb, n * 4));
+    CK(hipMalloc(&vb, n * 4));
+    CK(hipMalloc(&table, R * chunks * 4));
+    CK(hipMalloc(&bsums, 4096));
+    CK(hipMalloc(&stamps, chunks * 8 * 8));
+    CK(hipMalloc(&cdf, (1u << 20) * 4));
+    if (zipf) {  // the workload of tests/_util.py zipf_cdf_u32
+        std::vector<double> c(1u << 20);
+        double acc = 0;
+        for (uint32_t r = 0; r < (1u << 20); ++r) c[r] = (acc += 1.0 / (r + 1.0));
+        std::vector<uint32_t> t(1u << 20);
+        for (uint32_t r = 0; r < (1u << 20); ++r) t[r] = (uint32_t)fmin(floor(c[r] / acc * 4294967296.0), 4294967295.0);
+        t.back() = 0xFFFFFFFFu;
+        CK(hipMemcpy(cdf, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        rs_gen_zipf<<<65536, 256>>>(k0, n, 0x5EED, cdf, 1u << 20);
+    } else {
+        rs_gen_uniform<<<65536, 256>>>(k0, n, 0x5EED);
+    }
+    rs_gen_iota<<<65536, 256>>>(v0, n, 0);
+    CK(hipDeviceSynchronize());
+
+    auto table_for = [&](const uint32_t *keys, uint32_t shift) {
+        HistArgs h{};
+        h.keys = keys;
+        h.table = table;
+        h.n = n;
+        h.chunk_keys = chunk_keys;
+        h.num_chunks = chunks;
+        h.shift = shift;
+        h.vec = 1;
+        h.split = 1;
+        rs_histogram<8, 1024, kDigitShift, 1, 8><<<chunks, 1024>>>(h);
+        ScanArgs sa{};
+        sa.table = table;
+        sa.block_sums = bsums;
+        sa.m = (uint64_t)R * chunks;
+        sa.nblocks = (uint32_t)((sa.m + kScanSegment - 1) / kScanSegment);
+        rs_scan_reduce<<<sa.nblocks, kScanThreads>>>(sa);
+        rs_scan_down<<<sa.nblocks, kScanThreads>>>(sa);
+        CK(hipGetLastError());
+    };
+    auto args = [&](const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, uint32_t shift) {
+        ScatterArgs a{};
+        a.kin = ki;
+        a.vin = vi;
+        a.kout = ko;
+        a.vout = vo;
+        a.table = table;
+        a.n = n;
+        a.chunk_keys = chunk_keys;
+        a.num_chunks = chunks;
+        a.shift = shift;
+        return a;
+    };
+    const uint32_t *in_k = k0, *in_v = v0;
+    uint32_t shift = 0;
+    if (pass == 1) {  // pass 0 first (64-B kernel), into ka/va; time pass 1 on it
+        table_for(k0, 0);
+        rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2><<<chunks, 512>>>(args(k0, v0, ka, va, 0));
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(k0, ka, n * 4, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy(v0, va, n * 4, hipMemcpyDeviceToDevice));
+        shift = 8;
+    }
+    table_for(in_k, shift);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char *name, auto launch) {
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < reps; ++i) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipGetLastError());
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("%-44s %8.3f ms/pass  %6.1f GB/s (%.3f of 8 TB/s)\n", name, ms / reps, 16.0 * n / (ms / reps) / 1e6,
+               16.0 * n / (ms / reps) / 1e6 / 8000.0);
+        fflush(stdout);
+    };
+    printf("2^%d pairs, %s keys, pass %d, %u chunks x %llu tiles\n", lg, zipf ? "Zipf" : "uniform", pass, chunks,
+           (unsigned long long)tpc);
+    timeit("rs_scatter_lines pairs (64-B lines)", [&] {
+        rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2><<<chunks, 512>>>(args(in_k, in_v, ka, va, shift));
+    });
+    timeit("rs_scatter_lines pairs (64-B lines), CL", [&] {
+        rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1><<<chunks, 512>>>(args(in_k, in_v, ka, va, shift));
+    });
+    ScatterArgs sb = args(in_k, in_v, kb, vb, shift);
+    sb.stamps = stamps;
+    timeit("rs_scatter_pairs (128-B lines)", [&] { rs_scatter_pairs<8, 512, 16><<<chunks, 512>>>(sb); });
+    std::vector<unsigned long long> st(chunks * 8);
+    CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> st1 = st;
+    const bool eq_k = [&] {
+        std::vector<uint32_t> a(n), b(n);
+        CK(hipMemcpy(a.data(), ka, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), kb, n * 4, hipMemcpyDeviceToHost));
+        if (memcmp(a.data(), b.data(), n * 4)) return false;
+        CK(hipMemcpy(a.data(), va, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), vb, n * 4, hipMemcpyDeviceToHost));
+        return memcmp(a.data(), b.data(), n * 4) == 0;
+    }();
+    printf("  outputs equal: %s\n", eq_k ? "yes" : "NO");
+    timeit("rs_scatter_pairs (128-B lines), CL", [&] { rs_scatter_pairs<8, 512, 16, 1><<<chunks, 512>>>(sb); });
+    timeit("rs_scatter_pairs (128-B lines), PF=2", [&] { rs_scatter_pairs<8, 512, 16, 0, 2><<<chunks, 512>>>(sb); });
+    CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    printf("  PF=2 cycles per tile:");
+    for (int i = 0; i < 5; ++i) {
+        double s2 = 0;
+        for (uint32_t c = 0; c < chunks; ++c) s2 += (double)st[c * 8 + i];
+        printf("  %.0f", s2 / chunks / tpc);
+    }
+    printf("\n");
+    {
+        std::vector<uint32_t> x(n), y(n);
+        CK(hipMemcpy(x.data(), ka, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), kb, n * 4, hipMemcpyDeviceToHost));
+        const bool e1 = memcmp(x.data(), y.data(), n * 4) == 0;
+        CK(hipMemcpy(x.data(), va, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), vb, n * 4, hipMemcpyDeviceToHost));
+        printf("  PF=2 outputs equal: %s\n", e1 && memcmp(x.data(), y.data(), n * 4) == 0 ? "yes" : "NO");
+    }
+    timeit("rs_scatter_pairs (128-B lines), PF=2, CL", [&] { rs_scatter_pairs<8, 512, 16, 1, 2><<<chunks, 512>>>(sb); });
+    const char *ph[] = {"rank+load wait", "segments+carry", "line records", "staging", "output", "", "", ""};
+    printf("  rs_scatter_pairs cycles per tile (thread 0, mean over chunks):");
+    for (int i = 0; i < 5; ++i) {
+        double s = 0;
+        for (uint32_t c = 0; c < chunks; ++c) s += (double)st1[c * 8 + i];
+        printf("  %s %.0f", ph[i], s / chunks / tpc);
+    }
+    printf("\n");
+    return eq_k ? 0 : 3;
+}

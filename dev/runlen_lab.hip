@@ -1,3 +1,4 @@
+// Backs DESIGN §3 "Whole-line writes" and §8: the HBM floor of the scatter write stream vs run length and offset (128-B runs 1.67 ms per 2^30 keys; pairs: 128-B runs 2.90 ms, 64-B offset 3.74 ms).
 // runlen_lab.hip -- development harness: HBM cost of an LSD-scatter-shaped write stream as a
 // function of the run length. A persistent grid walks chunks of 16384-key tiles; each tile is read
 // with coalesced 16-B loads and written as T/L runs of L keys (16-B stores, whole aligned lines),

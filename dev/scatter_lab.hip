@@ -1,3 +1,4 @@
+// Backs DESIGN §3: scatter-kernel variants and ceilings (non-temporal loads/stores, LAB_PAIRS / LAB_K4 / LAB_SHAPE rows, the 4096-key vs 16384-key tiles).
 // scatter_lab.hip -- development harness (not part of the library): times variants of the
 // fused local-sort + scatter kernel and HBM ceilings on the current GPU, and checks every
 // variant's pass output against the first variant's (the pass output is unique).

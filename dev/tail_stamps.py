@@ -1,3 +1,4 @@
+# Backs DESIGN §3 tail_scan row: the timeline of a tail-scanned C2 pass (s_memrealtime stamps).
 """dev/tail_stamps.py -- with the stamps variant of the library (dev/build_variant.sh tstamp2 ...), the
 timeline of the last tail-scanned pass at C2 (s_memrealtime, 100 MHz): first workgroup start, last
 workgroup's end of work, tail start, tail end."""

@@ -1,3 +1,4 @@
+// Backs rsort_kernels.hip rs_scatter_lines header: partial-line writes cost as much as whole lines (1.7 ms aligned vs 2.8 ms misaligned).
 // wc_lab.hip -- development harness: which cache policy / granularity makes the LSD scatter's
 // partial-line writes cheap. Synthetic run scatter (as in write_lab.hip): chunk c walks tiles of
 // T = THREADS*KPT keys; key i of a tile goes to region d = i / L at

@@ -17,9 +17,9 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -- \
-    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu --no-vendor --no-e2e $ARGS > "$OUT/bench_trace.log" 2>&1 &&
+    python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu --no-vendor --no-e2e --configs "" $ARGS > "$OUT/bench_trace.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --no-vendor --no-e2e $ARGS > "$OUT/bench_fetch.log" 2>&1 &&
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --no-vendor --no-e2e --configs "" $ARGS > "$OUT/bench_fetch.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -- \
-    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --no-vendor --no-e2e $ARGS > "$OUT/bench_write.log" 2>&1
+    python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --no-vendor --no-e2e --configs "" $ARGS > "$OUT/bench_write.log" 2>&1
 echo "profiles written to $OUT"
