@@ -82,6 +82,13 @@ int hip_status(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP
 
 bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
 
+// The whole-line scatter kernels can write these outputs: any 4-B-aligned kout (launch_scatter
+// counts positions from its 128-B-aligned base); values at a multiple of 16 B from the keys.
+bool line_capable(const void *kout, const void *vout, int pairs) {
+    if (!aligned4(kout)) return false;
+    return !pairs || ((((uintptr_t)vout - (uintptr_t)kout) & 15u) == 0);
+}
+
 // ------------------------------------------------------------------------------ planning
 int device_cus() {
     int dev = 0, count = 0, c = 0;
@@ -125,7 +132,7 @@ bool joint_plan(const rsort_plan &p) {
 
 // Next-digit counts (rs_scatter_lines, k = 3, 4 keys): each pass adds the next pass's chunk table
 // from where it writes every key, so only pass 0 reads keys for a histogram. Needs the line
-// kernel (lane-ordered ranks, 16-B aligned outputs: checked per sort) and a second table.
+// kernel (lane-ordered ranks, line-capable outputs: checked per sort) and a second table.
 bool next_plan(const rsort_plan &p) {
     const int g = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 && (g == kGeomSmall || g == kGeomLines);
@@ -344,7 +351,7 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     const int rank = internal_rank((dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH);
     const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
-    const int aligned16 = ((((uintptr_t)kout) | (p.pairs ? (uintptr_t)vout : 0u)) & 15u) == 0;
+    const int aligned16 = line_capable(kout, vout, p.pairs);
     if ((bounds || next_table) && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
         return RSORT_ERR_ARG;  // group chunks, next-digit counts: rs_scatter_lines only
     PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
@@ -391,15 +398,14 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // digit-group chunks on every second pass (joint_plan): needs rs_scatter_lines for both
     // outputs (lane-ordered ranks, 16-B aligned ping-pong buffers)
     const bool joint = joint_plan(p) && g_group_chunks.load() != 0 &&
-                       internal_rank(g_rank_algo.load()) == kRankAtomic &&
-                       ((((uintptr_t)kout) | (uintptr_t)c.tmp_k |
-                         (p.pairs ? ((uintptr_t)vout | (uintptr_t)c.tmp_v) : 0u)) & 15u) == 0;
+                       internal_rank(g_rank_algo.load()) == kRankAtomic && line_capable(kout, vout, p.pairs) &&
+                       line_capable(c.tmp_k, c.tmp_v, p.pairs);
     if (joint_plan(p) && !joint &&
         hipMemsetAsync(c.bounds, 0, (size_t)2 * kBoundsWords * 4, s) != hipSuccess)  // rsort_group_flags: none
         return RSORT_ERR_HIP;
     // next-digit counts (k = 3, 4): the same kernel conditions as digit groups
     const bool nextc = next_plan(p) && g_group_chunks.load() != 0 && internal_rank(g_rank_algo.load()) == kRankAtomic &&
-                       ((((uintptr_t)kout) | (uintptr_t)c.tmp_k) & 15u) == 0;
+                       line_capable(kout, nullptr, 0) && line_capable(c.tmp_k, nullptr, 0);
     if (next_plan(p) && !nextc && hipMemsetAsync(c.done, 0, 8, s) != hipSuccess)  // rsort_plan_check: clean
         return RSORT_ERR_HIP;
     for (int i = 0; i < P; ++i) {

@@ -115,6 +115,10 @@ struct ScatterArgs {
     // variant (rank_add_hot); *cl_select == kGroupsWhole runs the plain one, anything else (a pass
     // whose digit groups were unbalanced: skewed, duplicate-heavy keys) the clustered one
     const uint32_t *cl_select;
+    // whole-line kernels only (set by launch_scatter): kout / vout are moved down to kout's 128-B-
+    // aligned base and every output position up by pos_shift (< 32) keys, so lines are cache lines
+    // for any 4-B-aligned output
+    uint32_t pos_shift;
 };
 
 struct ScanArgs {
@@ -169,8 +173,9 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
                                uint32_t snap, hipStream_t s);
-// rank_algo: internal RankAlgo. aligned16: kout/vout 16-B aligned (kGeomLines line stores;
-// otherwise the same plan runs rs_scatter with the same tiles).
+// rank_algo: internal RankAlgo. aligned16: the whole-line kernels may run -- keys-only: always
+// (any 4-B-aligned kout; launch_scatter shifts positions to kout's 128-B-aligned base); pairs: when
+// (vout - kout) % 16 == 0 (otherwise the same plan runs rs_scatter with the same tiles).
 hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geom, int aligned16,
                           const ScatterArgs &a, hipStream_t s);
 // Whether a (bits, pairs, rank_algo, dmode, geom) scatter kernel is compiled in.

@@ -56,11 +56,20 @@ namespace rsort {
 namespace {
 std::mutex g_kn_mu;
 std::vector<std::pair<const void *, std::string>> g_kn_names;  // every registered kernel
+std::vector<const void *> g_kn_lines;                           // ... of them the whole-line kernels
 std::vector<const void *> g_kn_used;                           // launched since the last reset
 
-void register_kernel(const void *fn, const char *name) {
+void register_kernel(const void *fn, const char *name, bool lines = false) {
     std::lock_guard<std::mutex> g(g_kn_mu);
     g_kn_names.emplace_back(fn, std::string(name));
+    if (lines) g_kn_lines.push_back(fn);
+}
+
+bool is_line_kernel(const void *fn) {
+    std::lock_guard<std::mutex> g(g_kn_mu);
+    for (const void *x : g_kn_lines)
+        if (x == fn) return true;
+    return false;
 }
 
 void note_used(const void *fn) {
@@ -1318,7 +1327,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     const uint32_t glead = lane & ~(TPD - 1u);
     uint32_t g_run = 0, carry = 0, inv = 0;
     if (leader) {
-        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
+        // positions relative to kout's 128-B-aligned base (ScatterArgs::pos_shift): lines are cache lines
+        const uint32_t g0 = a.table[(uint64_t)d_own * a.num_chunks + c];
+        const uint32_t g = g0 + a.pos_shift;
         carry = g & (G - 1u);  // the first line starts before the chunk's output
         inv = carry;
         g_run = g;
@@ -1331,7 +1342,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         for (uint32_t x = 0; x < inv; ++x) s_stage[CAP + d_own * G + x] = ik;
         if constexpr (NX) {
             if (count_next) {
-                const uint64_t oc = (uint64_t)g / a.chunk_keys;
+                const uint64_t oc = (uint64_t)g0 / a.chunk_keys;  // (the next pass's chunks: unshifted)
                 s_oc[d_own] = (uint32_t)oc;
                 s_nb[d_own] = (uint32_t)min<uint64_t>((oc + 1) * a.chunk_keys, 0xFFFFFFFFull);
             }
@@ -1380,7 +1391,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         if constexpr (NX) {
             if (count_next) {
                 // a quad never straddles a chunk boundary (both are multiples of 4 keys)
-                const uint32_t slot = (uint32_t)gp >= s_nb[d] ? 1u : 0u;
+                const uint32_t slot = (uint32_t)gp - a.pos_shift >= s_nb[d] ? 1u : 0u;
 #pragma unroll
                 for (uint32_t x = 0; x < 4; ++x)
                     if (lo <= q + x) next_add(d, slot, kv[x]);
@@ -1629,7 +1640,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_vstage[CAP + item];
                 if constexpr (NX) {
                     const uint32_t d = item / G;
-                    if (count_next) next_add(d, fl.x + x >= s_nb[d] ? 1u : 0u, k);
+                    if (count_next) next_add(d, fl.x + x - a.pos_shift >= s_nb[d] ? 1u : 0u, k);
                 }
             }
         }
@@ -1753,7 +1764,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     // invalid leading slots of the chunk's first line; carry slots sub * CPT .. + CPT - 1 in ck / cv
     uint32_t g_run, carry, inv;
     {
-        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c];
+        const uint32_t g = a.table[(uint64_t)d_own * a.num_chunks + c] + a.pos_shift;  // (as rs_scatter_lines)
         carry = g & (G - 1u);
         inv = carry;
         g_run = g;
@@ -2137,7 +2148,7 @@ static void *reg_lines() {
         char nm[96];
         snprintf(nm, sizeof nm, "rs_scatter_lines<%d, %d, %d, %d, %s, %d, %d, %d>", BITS, THREADS, KPT, G,
                  PAIRS ? "true" : "false", DMODE, NT, CL);
-        register_kernel(fn, nm);
+        register_kernel(fn, nm, true);
         return true;
     }();
     (void)once;
@@ -2150,7 +2161,7 @@ static void *reg_pairs() {
     static const bool once = [fn] {
         char nm[96];
         snprintf(nm, sizeof nm, "rs_scatter_pairs<%d, %d, %d, %d>", BITS, THREADS, KPT, CL);
-        register_kernel(fn, nm);
+        register_kernel(fn, nm, true);
         return true;
     }();
     (void)once;
@@ -2461,6 +2472,15 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
+    if (is_line_kernel(fn)) {
+        // whole-line kernels write cache lines: positions count from kout's 128-B-aligned base, the
+        // slots before kout are masked like any chunk's leading slots (values: the same shift; the
+        // caller checked (vout - kout) % 16 == 0, so vout's base stays 16-B aligned)
+        const uintptr_t ko = (uintptr_t)a.kout, sh = ko & 127u;
+        copy.kout = reinterpret_cast<uint32_t *>(ko - sh);
+        if (pairs) copy.vout = reinterpret_cast<uint32_t *>((uintptr_t)a.vout - sh);
+        copy.pos_shift = (uint32_t)(sh / 4u);
+    }
     note_used(fn);
     if (cl != nullptr) note_used(cl);
     void *args[] = {&copy};

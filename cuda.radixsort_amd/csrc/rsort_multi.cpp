@@ -100,6 +100,45 @@ size_t multi_bytes(int64_t n, int64_t cap, int k, int pairs, int world, MultiCar
 
 int hip_st(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP; }
 
+// A second stream per device (with its two events) for work that overlaps the exchange: created on
+// first use, kept for the process. Concurrent multi-GPU sorts on one device (the loopback tests'
+// ranks) each take their own from a small pool.
+struct SideStream {
+    int device;
+    bool busy;
+    hipStream_t s;
+    hipEvent_t ready, done;
+};
+std::mutex g_side_mu;
+std::vector<SideStream *> g_side;
+
+SideStream *side_stream() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_side_mu);
+    for (SideStream *x : g_side)
+        if (x->device == dev && !x->busy) {
+            x->busy = true;
+            return x;
+        }
+    SideStream *x = new (std::nothrow) SideStream{dev, true, nullptr, nullptr, nullptr};
+    if (!x) return nullptr;
+    if (hipStreamCreateWithFlags(&x->s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x->ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+        delete x;  // (a partly created stream/event leaks: a HIP failure this early is terminal anyway)
+        return nullptr;
+    }
+    g_side.push_back(x);
+    return x;
+}
+
+void side_release(SideStream *x) {
+    if (!x) return;
+    std::lock_guard<std::mutex> g(g_side_mu);
+    x->busy = false;
+}
+
 // ------------------------------------------------------------------------------ RCCL transport
 struct RcclCtx {
     ncclComm_t comm;
@@ -272,6 +311,20 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     else if (workspace_bytes < need) local = RSORT_ERR_WORKSPACE;
     if (local != RSORT_OK) n = 0;  // (nothing below reads the keys of a failed rank)
     int st;
+    if (world == 1) {
+        // one rank: the partition would be one bucket (a copy) and the exchange a self copy, so the
+        // keys go straight through the local sort (same output, no peers to agree with)
+        if (local != RSORT_OK) return local;
+        if (n > capacity) return RSORT_ERR_CAPACITY;
+        if (n > 0) {
+            rsort_plan p;
+            if ((st = rsort_plan_make(n, k_bits, pairs, 0, &p))) return st;
+            if ((st = rsort_sort_planned(&p, d_keys, d_vals, d_keys_out, d_vals_out, m.sub, m.sub_bytes, s))) return st;
+        }
+        *out_n = n;
+        *out_offset = 0;
+        return RSORT_OK;
+    }
     auto first_status = [&](const uint64_t *words, size_t stride, size_t at) {
         for (int r = 0; r < world; ++r)
             if (words[(size_t)r * stride + at] != 0) return (int)words[(size_t)r * stride + at];
@@ -362,15 +415,31 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     rsort_exchange_plan xp;
     if ((st = rsort_multi_exchange_plan(world, me, buckets, counts, &spl, caps, &xp))) return st;
 
-    // 5. the exchange: own range by a device copy, the rest in equal rounds of <= the piece limit
+    // 5. the exchange: own range by a device copy on a side stream (it overlaps the messages, which
+    //    the transport moves on `s`; joined before the local sort), the rest in equal rounds of <=
+    //    the piece limit
     if (xp.send_cnt[me] != xp.recv_cnt[me]) return RSORT_ERR_ARG;
+    SideStream *side = nullptr;
+    struct SideGuard {
+        SideStream *&x;
+        ~SideGuard() { side_release(x); }  // (waits already enqueued keep the events' state)
+    } side_guard{side};
     if (xp.send_cnt[me] > 0) {
+        side = side_stream();
+        hipStream_t cs = s;
+        if (side && hipEventRecord(side->ready, s) == hipSuccess && hipStreamWaitEvent(side->s, side->ready, 0) == hipSuccess) {
+            cs = side->s;
+        } else {
+            side_release(side);
+            side = nullptr;
+        }
         if (hipMemcpyAsync(d_keys_out + xp.recv_off[me], m.part_k + xp.send_off[me], (size_t)xp.send_cnt[me] * 4,
-                           hipMemcpyDeviceToDevice, s) != hipSuccess)
+                           hipMemcpyDeviceToDevice, cs) != hipSuccess)
             return RSORT_ERR_HIP;
         if (pairs && hipMemcpyAsync(d_vals_out + xp.recv_off[me], m.part_v + xp.send_off[me],
-                                    (size_t)xp.send_cnt[me] * 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                                    (size_t)xp.send_cnt[me] * 4, hipMemcpyDeviceToDevice, cs) != hipSuccess)
             return RSORT_ERR_HIP;
+        if (side && hipEventRecord(side->done, side->s) != hipSuccess) return RSORT_ERR_HIP;
     }
     int64_t rounds = 0, piece = 0;
     exchange_rounds(xp.max_message, g_piece.load(), &rounds, &piece);
@@ -391,6 +460,8 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
             if ((st = tr->exchange(tr->ctx, sp_, sb, rp_, rb, s))) return st;
         }
     }
+
+    if (side && hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
 
     // 6. local sort of what arrived, in place (no collective follows: a failure here is this rank's)
     if (xp.n_recv > 0) {

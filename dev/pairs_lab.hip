@@ -177,6 +177,25 @@ int main(int argc, char **argv) {
         printf("  PF=2 outputs equal: %s\n", e1 && memcmp(x.data(), y.data(), n * 4) == 0 ? "yes" : "NO");
     }
     timeit("rs_scatter_pairs (128-B lines), PF=2, CL", [&] { rs_scatter_pairs<8, 512, 16, 1, 2><<<chunks, 512>>>(sb); });
+    timeit("rs_scatter_pairs 1024 x 8", [&] { rs_scatter_pairs<8, 1024, 8><<<chunks, 1024>>>(sb); });
+    CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
+    printf("  1024 x 8 cycles per tile:");
+    for (int i = 0; i < 5; ++i) {
+        double s2 = 0;
+        for (uint32_t c = 0; c < chunks; ++c) s2 += (double)st[c * 8 + i];
+        printf("  %.0f", s2 / chunks / tpc);
+    }
+    printf("\n");
+    {
+        std::vector<uint32_t> x(n), y(n);
+        CK(hipMemcpy(x.data(), ka, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), kb, n * 4, hipMemcpyDeviceToHost));
+        const bool e1 = memcmp(x.data(), y.data(), n * 4) == 0;
+        CK(hipMemcpy(x.data(), va, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), vb, n * 4, hipMemcpyDeviceToHost));
+        printf("  1024 x 8 outputs equal: %s\n", e1 && memcmp(x.data(), y.data(), n * 4) == 0 ? "yes" : "NO");
+    }
+    timeit("rs_scatter_pairs 1024 x 8, CL", [&] { rs_scatter_pairs<8, 1024, 8, 1><<<chunks, 1024>>>(sb); });
     const char *ph[] = {"rank+load wait", "segments+carry", "line records", "staging", "output", "", "", ""};
     printf("  rs_scatter_pairs cycles per tile (thread 0, mean over chunks):");
     for (int i = 0; i < 5; ++i) {

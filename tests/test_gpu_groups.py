@@ -264,8 +264,9 @@ def test_in_place_on_groups():
     assert np.array_equal(rs.to_numpy_u32(d), oracle_sort(x, 8))
 
 
-def test_unaligned_output_falls_back():
-    """An output buffer that is not 16-B aligned cannot take the whole-line kernel: fixed chunks."""
+def test_unaligned_output_keeps_groups():
+    """An output buffer that is 4-B but not 16-B aligned still takes the whole-line kernels (positions
+    from its 128-B-aligned base): digit groups on both odd passes."""
     n = 512 * LINE_TILE
     x = uniform_keys(n, seed=12)
     p = group_plan(n)
@@ -274,8 +275,24 @@ def test_unaligned_output_falls_back():
     d_out = big[1:]
     ws = rs.workspace(p.workspace_bytes)
     rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
-    assert rs.group_flags(p, ws) == [0, 0]
+    assert rs.group_flags(p, ws) == [1, 1]
     assert np.array_equal(rs.to_numpy_u32(d_out), oracle_sort(x, 8))
+
+
+def test_pairs_mismatched_alignment_falls_back():
+    """Pairs whose values sit at other than a multiple of 16 B from the keys cannot take the
+    whole-line kernels: fixed chunks, the same result."""
+    n = 512 * LINE_TILE
+    x = zipf_keys(n, seed=13)
+    v = np.arange(n, dtype=np.uint32)
+    p = rs.plan(n, 8, True)
+    ws = rs.workspace(p.workspace_bytes)
+    bigv = rs.empty_u32(n + 1)
+    ko, vo = rs.empty_u32(n), bigv[1:]
+    rs.sort_device(rs.from_numpy_u32(x), ko, 8, vals_in=rs.from_numpy_u32(v), vals_out=vo, ws=ws, plan_=p)
+    assert rs.group_flags(p, ws) == [0, 0]
+    rk, rv = oracle_sort_pairs(x, v, 8)
+    assert np.array_equal(rs.to_numpy_u32(ko), rk) and np.array_equal(rs.to_numpy_u32(vo), rv)
 
 
 # ------------------------------------------------------------------ next-digit counts (k = 3, 4)

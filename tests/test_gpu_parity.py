@@ -141,22 +141,60 @@ def test_whole_line_scatter(dist, tpc):
         assert np.array_equal(gpu_sort(x, k, tiles_per_chunk=tpc), oracle_sort(x, k)), (dist, tpc, k)
 
 
-def test_whole_line_scatter_misaligned_output_falls_back():
-    """An output pointer that is 4-B but not 16-B aligned takes the same tiles through
-    rs_scatter (no 16-B line stores); the result is the same."""
+def test_whole_line_scatter_unaligned_output():
+    """An output pointer that is 4-B but not 16-B aligned keeps the whole-line kernels: positions
+    count from its 128-B-aligned base (ScatterArgs::pos_shift) and the slots before it are masked,
+    so k = 8 (1024 x 16 line tiles), k = 4 (next-digit counts) and k = 3 all write whole cache
+    lines into any 4-B-aligned buffer; bit-exact."""
     n = (1 << 23) + 77
     x = zipf_keys(n, seed=5)
-    big = rs.empty_u32(n + 4)
-    for off in (1, 2, 3):
+    big = rs.empty_u32(n + 64)
+    for k in (8, 4, 3):
+        ref = oracle_sort(x, k)
+        for off in (1, 2, 3, 17, 31):
+            out = big[off:off + n]
+            rs.scatter_kernels_used(reset=True)
+            rs.sort_device(dev(x), out, k)
+            torch.cuda.synchronize()
+            assert np.array_equal(host(out), ref), (k, off)
+            assert all(u.startswith("rs_scatter_lines") for u in rs.scatter_kernels_used(reset=True)), (k, off)
+
+
+def test_unaligned_output_leaves_neighbours_untouched():
+    """The masked slots before an unaligned output and after its end stay as they were."""
+    n = (1 << 22) + 5
+    x = uniform_keys(n, seed=55)
+    for off in (1, 13, 30):
+        big = torch.full((n + 96,), -7, dtype=torch.int32, device="cuda")
         out = big[off:off + n]
         rs.sort_device(dev(x), out, 8)
         torch.cuda.synchronize()
-        assert np.array_equal(host(out), oracle_sort(x, 8)), off
+        h = host(big)
+        assert np.array_equal(h[off:off + n], oracle_sort(x, 8))
+        assert (h[:off] == np.uint32(0xFFFFFFF9)).all() and (h[off + n:] == np.uint32(0xFFFFFFF9)).all(), off
+
+
+def test_pairs_values_misaligned_against_keys_falls_back():
+    """Pairs need (vout - kout) % 16 == 0 for the whole-line kernels (keys and values share the
+    line positions); otherwise the same tiles go through rs_scatter. Same result either way."""
+    n = (1 << 23) + 19
+    x = zipf_keys(n, seed=6)
+    vals = np.arange(n, dtype=np.uint32)
+    rk, rv = oracle_sort_pairs(x, vals, 8)
+    bigk, bigv = rs.empty_u32(n + 8), rs.empty_u32(n + 8)
+    for ko, vo, lines in ((0, 1, False), (3, 3, True), (2, 6, True), (5, 2, False)):
+        out, vout = bigk[ko:ko + n], bigv[vo:vo + n]
+        rs.scatter_kernels_used(reset=True)
+        rs.sort_device(dev(x), out, 8, vals_in=dev(vals), vals_out=vout)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(out), rk) and np.array_equal(host(vout), rv), (ko, vo)
+        used = rs.scatter_kernels_used(reset=True)
+        assert any(u.startswith("rs_scatter_pairs") or u.startswith("rs_scatter_lines") for u in used) == lines, used
 
 
 def test_whole_line_scatter_16b_aligned_output():
-    """A 16-B but not 128-B aligned output keeps the line kernel (its lines then straddle the
-    L2 lines: slower, same result); keys and pairs."""
+    """A 16-B but not 128-B aligned output keeps the line kernel (positions shifted to the
+    128-B-aligned base, so its lines are still whole L2 lines); keys and pairs."""
     n = (1 << 23) + 333
     x = zipf_keys(n, seed=9)
     vals = np.arange(n, dtype=np.uint32)
