@@ -73,6 +73,12 @@ def parse():
     ap.add_argument("--dist-path", action="store_true",
                     help="run the multi-GPU sort (partition, RCCL all-to-all, local sort) even on one "
                          "rank: its overhead against the single-GPU sort")
+    ap.add_argument("--dist-full", action="store_true",
+                    help="multi-GPU step (c): the whole protocol also at one rank (RSORT_MULTI_FULL: sample, "
+                         "partition, self exchange); by default one rank sorts directly")
+    ap.add_argument("--dist-overlap", action="store_true",
+                    help="multi-GPU step (c): RSORT_MULTI_OVERLAP (sort each rank's lower half while the upper "
+                         "half is exchanged)")
     ap.add_argument("--primitives", action="store_true",
                     help="time the pass primitives in isolation instead (SURVEY 8f row 3) and exit")
     ap.add_argument("--no-group-chunks", action="store_true",
@@ -362,6 +368,7 @@ def main():
 
     comm = None
     if use_dist and a.dist_impl == "c":
+        rs.set_multi_options((rs.MULTI_FULL if a.dist_full else 0) | (rs.MULTI_OVERLAP if a.dist_overlap else 0))
         uid = [rs.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         with stdout_to_stderr():
@@ -559,7 +566,9 @@ def main():
                                    else "wave64 ballot peer match (kRankCount)" if a.rank == "match"
                                    else "k 1-bit splits (kRankSplit)"),
                        "parallelism": "single GPU" if not use_dist else
-                       f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'})"},
+                       f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'}"
+                       f"{', overlap' if a.dist_overlap and a.dist_impl == 'c' else ''}"
+                       f"{', full protocol' if a.dist_full and a.dist_impl == 'c' else ''})"},
             "verified": bool(verified),
             "roofline": roof,
             "phases_ms_per_step": {"histogram": round(hi["ms"] / a.steps, 4), "scan": round(scan["ms"] / a.steps, 4),

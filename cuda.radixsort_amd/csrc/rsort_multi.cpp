@@ -43,6 +43,7 @@ constexpr int64_t kSampleBudget = (int64_t)1 << 20;
 // messages arrive whole
 constexpr int64_t kMaxPiece = (int64_t)1 << 28;
 std::atomic<int64_t> g_piece{kMaxPiece};  // rsort_set_exchange_piece (tests force several rounds)
+std::atomic<int> g_multi_opts{0};         // rsort_set_multi_options
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -63,7 +64,8 @@ struct MultiCarve {
 int64_t samples_per_rank(int world) { return std::max<int64_t>(1, kSampleBudget / world); }
 
 size_t sub_bytes(int64_t n, int64_t cap, int k, int pairs, int world) {
-    size_t a = rsort_partition_workspace_size(n, std::min(2 * world - 1, kMaxSplitters + 1), pairs);
+    (void)world;
+    size_t a = rsort_partition_workspace_size(n, kMaxSplitters + 1, pairs);  // (any bucket count: overlap mode)
     // the gathered sample: world rows of at most kSampleBudget samples
     size_t b = rsort_workspace_size(world * kSampleBudget, 8, 0) + ((size_t)4 << 8 << 12);
     // the received count is only known later; a smaller n can pick a geometry with a larger
@@ -311,7 +313,8 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     else if (workspace_bytes < need) local = RSORT_ERR_WORKSPACE;
     if (local != RSORT_OK) n = 0;  // (nothing below reads the keys of a failed rank)
     int st;
-    if (world == 1) {
+    const int opts = g_multi_opts.load();
+    if (world == 1 && !(opts & RSORT_MULTI_FULL)) {
         // one rank: the partition would be one bucket (a copy) and the exchange a self copy, so the
         // keys go straight through the local sort (same output, no peers to agree with)
         if (local != RSORT_OK) return local;
@@ -325,6 +328,11 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         *out_offset = 0;
         return RSORT_OK;
     }
+    // RSORT_MULTI_OVERLAP: every rank's key range is cut in two (H = 2 virtual ranks per rank, the
+    // planning functions run for world * H ranks); the lower half is exchanged first and sorted on a
+    // side stream while the upper half is exchanged
+    const int H = ((opts & RSORT_MULTI_OVERLAP) && world >= 2 && 2 * world <= kMaxRanks) ? 2 : 1;
+    const int V = world * H;
     auto first_status = [&](const uint64_t *words, size_t stride, size_t at) {
         for (int r = 0; r < world; ++r)
             if (words[(size_t)r * stride + at] != 0) return (int)words[(size_t)r * stride + at];
@@ -340,23 +348,23 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     uint64_t nf[kNWords * kMaxRanks];
     if ((st = d2h(nf, m.n_all, (size_t)world * sizeof(mine), s))) return st;
     if ((st = first_status(nf, kNWords, 2))) return st;
-    int64_t n_all[kMaxRanks];
+    int64_t n_all[kMaxRanks] = {0};  // per virtual rank: rank r's keys at r * H, none at the others
     bool any_pairs = false, bad = false;
     for (int r = 0; r < world; ++r) {
-        n_all[r] = (int64_t)nf[kNWords * r];
+        n_all[r * H] = (int64_t)nf[kNWords * r];
         any_pairs |= (nf[kNWords * r + 1] & 1) != 0;
     }
     for (int r = 0; r < world && any_pairs; ++r)
-        bad |= !(nf[kNWords * r + 1] & 4) || (n_all[r] > 0 && !(nf[kNWords * r + 1] & 2));
+        bad |= !(nf[kNWords * r + 1] & 4) || ((int64_t)nf[kNWords * r] > 0 && !(nf[kNWords * r + 1] & 2));
     if (bad) return RSORT_ERR_ARG;
     rsort_sample_plan sp;
-    if ((st = rsort_multi_sample_plan(world, n_all, samples_per_rank(world), &sp))) return st;
-    if (sp.row_len > kSampleBudget) return RSORT_ERR_ARG;  // cannot happen: budget / world per rank
+    if ((st = rsort_multi_sample_plan(V, n_all, samples_per_rank(V), &sp))) return st;
+    if (sp.row_len > kSampleBudget) return RSORT_ERR_ARG;  // cannot happen: budget / V per virtual rank
 
     // 2. sample (+ this rank's status in the row's last word), gather, sort on the device, read
     //    the quantile keys
     const size_t row = (size_t)sp.row_len + 1;
-    if (launch_sample(d_keys, (uint64_t)n, (uint64_t)sp.stride, (uint64_t)sp.count[me], (uint64_t)sp.row_len,
+    if (launch_sample(d_keys, (uint64_t)n, (uint64_t)sp.stride, (uint64_t)sp.count[me * H], (uint64_t)sp.row_len,
                       m.samp_send, s) != hipSuccess)
         local = RSORT_ERR_HIP;
     const uint32_t lst = (uint32_t)local;
@@ -373,19 +381,19 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
             if (sts[r]) return (int)sts[r];
     }
     uint32_t q[kMaxRanks] = {0};
-    if (world > 1 && sp.total > 0) {
+    if (V > 1 && sp.total > 0) {
         // the rows (each followed by its status word) sorted as one array: the status words are 0
         // and sort first, so the quantile positions move up by world
         const int64_t ns = (int64_t)world * (int64_t)row;
         local = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s);
-        for (int i = 1; i < world && !local; ++i)
+        for (int i = 1; i < V && !local; ++i)
             if (hipMemcpyAsync(&q[i - 1], m.samp_all + world + rsort_multi_quantile_index(&sp, i), 4,
                                hipMemcpyDeviceToHost, s) != hipSuccess)
                 local = RSORT_ERR_HIP;
         if (!local && hipStreamSynchronize(s) != hipSuccess) local = RSORT_ERR_HIP;
     }
     rsort_multi_splitters spl;
-    if ((st = rsort_multi_splitters_make(world, q, &spl))) return st;  // pure, identical on every rank
+    if ((st = rsort_multi_splitters_make(V, q, &spl))) return st;  // pure, identical on every rank
 
     // 3. stable partition into the splitters' buckets
     const int buckets = spl.nsplit + 1;
@@ -396,7 +404,7 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
                                        m.sub_bytes, s);
     if (!local) local = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s);
 
-    // 4. count matrix + capacities + statuses -> exchange plan (the same on every rank)
+    // 4. count matrix + capacities + statuses -> the exchange plans (the same on every rank)
     uint64_t rowc[kMaxBuckets + 2];
     for (int b = 0; b < buckets; ++b) rowc[b] = local ? 0u : (uint64_t)(starts[b + 1] - starts[b]);
     rowc[buckets] = (uint64_t)capacity;
@@ -407,71 +415,102 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     uint64_t all[kMaxRanks * (kMaxBuckets + 2)];
     if ((st = d2h(all, m.c_all, (size_t)world * row_bytes, s))) return st;
     if ((st = first_status(all, (size_t)buckets + 2, (size_t)buckets + 1))) return st;
-    int64_t counts[kMaxRanks * kMaxBuckets], caps[kMaxRanks];
+    int64_t counts[kMaxRanks * kMaxBuckets] = {0}, caps[kMaxRanks], cap_of[kMaxRanks];
     for (int r = 0; r < world; ++r) {
-        for (int b = 0; b < buckets; ++b) counts[r * buckets + b] = (int64_t)all[r * (buckets + 2) + b];
-        caps[r] = (int64_t)all[r * (buckets + 2) + buckets];
+        for (int b = 0; b < buckets; ++b) counts[r * H * buckets + b] = (int64_t)all[r * (buckets + 2) + b];
+        cap_of[r] = (int64_t)all[r * (buckets + 2) + buckets];
+        for (int h = 0; h < H; ++h) caps[r * H + h] = cap_of[r];  // (the halves' sum is checked below)
     }
-    rsort_exchange_plan xp;
-    if ((st = rsort_multi_exchange_plan(world, me, buckets, counts, &spl, caps, &xp))) return st;
+    // every virtual rank's plan: this rank sends as virtual rank me * H and receives as me * H + h;
+    // the capacity check is on each rank's total
+    rsort_exchange_plan xv[kMaxRanks];
+    for (int v = 0; v < V; ++v) {
+        st = rsort_multi_exchange_plan(V, v, buckets, counts, &spl, caps, &xv[v]);
+        if (st != RSORT_OK && st != RSORT_ERR_CAPACITY) return st;
+    }
+    for (int r = 0; r < world; ++r) {
+        int64_t tot = 0;
+        for (int h = 0; h < H; ++h) tot += xv[r * H + h].n_recv;
+        if (tot > cap_of[r]) return RSORT_ERR_CAPACITY;
+    }
+    const rsort_exchange_plan &xs = xv[me * H];  // (all sends of this rank)
 
-    // 5. the exchange: own range by a device copy on a side stream (it overlaps the messages, which
-    //    the transport moves on `s`; joined before the local sort), the rest in equal rounds of <=
-    //    the piece limit
-    if (xp.send_cnt[me] != xp.recv_cnt[me]) return RSORT_ERR_ARG;
-    SideStream *side = nullptr;
+    // 5-6. per half: the exchange (the own range by a device copy on a side stream beside the
+    //      messages, which the transport moves on `s`; the rest in equal rounds of <= the piece
+    //      limit), then the local sort of what arrived, in place. With two halves the first half's
+    //      sort runs on the side stream while the second half is exchanged.
+    int64_t rounds = 0, piece = 0;
+    exchange_rounds(xs.max_message, g_piece.load(), &rounds, &piece);
+    SideStream *side = side_stream();
     struct SideGuard {
-        SideStream *&x;
+        SideStream *x;
         ~SideGuard() { side_release(x); }  // (waits already enqueued keep the events' state)
     } side_guard{side};
-    if (xp.send_cnt[me] > 0) {
-        side = side_stream();
-        hipStream_t cs = s;
-        if (side && hipEventRecord(side->ready, s) == hipSuccess && hipStreamWaitEvent(side->s, side->ready, 0) == hipSuccess) {
-            cs = side->s;
-        } else {
-            side_release(side);
-            side = nullptr;
-        }
-        if (hipMemcpyAsync(d_keys_out + xp.recv_off[me], m.part_k + xp.send_off[me], (size_t)xp.send_cnt[me] * 4,
-                           hipMemcpyDeviceToDevice, cs) != hipSuccess)
-            return RSORT_ERR_HIP;
-        if (pairs && hipMemcpyAsync(d_vals_out + xp.recv_off[me], m.part_v + xp.send_off[me],
-                                    (size_t)xp.send_cnt[me] * 4, hipMemcpyDeviceToDevice, cs) != hipSuccess)
-            return RSORT_ERR_HIP;
-        if (side && hipEventRecord(side->done, side->s) != hipSuccess) return RSORT_ERR_HIP;
-    }
-    int64_t rounds = 0, piece = 0;
-    exchange_rounds(xp.max_message, g_piece.load(), &rounds, &piece);
-    for (int64_t rd = 0; rd < rounds; ++rd) {
-        for (int arr = 0; arr < (pairs ? 2 : 1); ++arr) {
-            uint32_t *src = arr ? m.part_v : m.part_k;
-            uint32_t *dst = arr ? d_vals_out : d_keys_out;
-            void *sp_[kMaxRanks], *rp_[kMaxRanks];
-            size_t sb[kMaxRanks], rb[kMaxRanks];
-            for (int p = 0; p < world; ++p) {
-                const int64_t a0 = std::min(xp.send_cnt[p], rd * piece), a1 = std::min(xp.send_cnt[p], (rd + 1) * piece);
-                const int64_t b0 = std::min(xp.recv_cnt[p], rd * piece), b1 = std::min(xp.recv_cnt[p], (rd + 1) * piece);
-                sp_[p] = src + xp.send_off[p] + a0;
-                rp_[p] = dst + xp.recv_off[p] + b0;
-                sb[p] = p == me ? 0 : (size_t)(a1 - a0) * 4;
-                rb[p] = p == me ? 0 : (size_t)(b1 - b0) * 4;
+    int64_t base = 0;
+    bool side_pending = false;  // the side stream holds work `s` must wait for
+    for (int h = 0; h < H; ++h) {
+        const rsort_exchange_plan &xd = xv[me * H + h];
+        const int own_dst = me * H + h, own_src = me * H;
+        if (xs.send_cnt[own_dst] != xd.recv_cnt[own_src]) return RSORT_ERR_ARG;
+        uint32_t *ok = d_keys_out + base, *ov = pairs ? d_vals_out + base : nullptr;
+        const int64_t own = xs.send_cnt[own_dst];
+        if (own > 0) {
+            hipStream_t cs = s;
+            if (side && !side_pending && hipEventRecord(side->ready, s) == hipSuccess &&
+                hipStreamWaitEvent(side->s, side->ready, 0) == hipSuccess)
+                cs = side->s;
+            if (hipMemcpyAsync(ok + xd.recv_off[own_src], m.part_k + xs.send_off[own_dst], (size_t)own * 4,
+                               hipMemcpyDeviceToDevice, cs) != hipSuccess)
+                return RSORT_ERR_HIP;
+            if (pairs && hipMemcpyAsync(ov + xd.recv_off[own_src], m.part_v + xs.send_off[own_dst], (size_t)own * 4,
+                                        hipMemcpyDeviceToDevice, cs) != hipSuccess)
+                return RSORT_ERR_HIP;
+            if (cs != s) {
+                if (hipEventRecord(side->done, side->s) != hipSuccess) return RSORT_ERR_HIP;
+                side_pending = true;
             }
-            if ((st = tr->exchange(tr->ctx, sp_, sb, rp_, rb, s))) return st;
         }
+        for (int64_t rd = 0; rd < rounds; ++rd) {
+            for (int arr = 0; arr < (pairs ? 2 : 1); ++arr) {
+                uint32_t *src = arr ? m.part_v : m.part_k;
+                uint32_t *dst = arr ? ov : ok;
+                void *sp_[kMaxRanks], *rp_[kMaxRanks];
+                size_t sb[kMaxRanks], rb[kMaxRanks];
+                for (int p = 0; p < world; ++p) {
+                    const int dv = p * H + h, sv = p * H;  // virtual destination / source
+                    const int64_t a0 = std::min(xs.send_cnt[dv], rd * piece), a1 = std::min(xs.send_cnt[dv], (rd + 1) * piece);
+                    const int64_t b0 = std::min(xd.recv_cnt[sv], rd * piece), b1 = std::min(xd.recv_cnt[sv], (rd + 1) * piece);
+                    sp_[p] = src + xs.send_off[dv] + a0;
+                    rp_[p] = dst + xd.recv_off[sv] + b0;
+                    sb[p] = p == me ? 0 : (size_t)(a1 - a0) * 4;
+                    rb[p] = p == me ? 0 : (size_t)(b1 - b0) * 4;
+                }
+                if ((st = tr->exchange(tr->ctx, sp_, sb, rp_, rb, s))) return st;
+            }
+        }
+        // this half has arrived (on `s`, and its own range on the side stream)
+        if (side_pending) {
+            if (hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
+            side_pending = false;
+        }
+        if (xd.n_recv > 0) {
+            rsort_plan p;
+            if ((st = rsort_plan_make(xd.n_recv, k_bits, pairs, 0, &p))) return st;
+            hipStream_t ss = s;
+            if (h + 1 < H && side && hipEventRecord(side->ready, s) == hipSuccess &&
+                hipStreamWaitEvent(side->s, side->ready, 0) == hipSuccess)
+                ss = side->s;  // sorted while the next half is exchanged on `s`
+            if ((st = rsort_sort_planned(&p, ok, ov, ok, ov, m.sub, m.sub_bytes, ss))) return st;
+            if (ss != s) {
+                if (hipEventRecord(side->done, side->s) != hipSuccess) return RSORT_ERR_HIP;
+                side_pending = true;  // (the next half's own copy then stays on `s`)
+            }
+        }
+        base += xd.n_recv;
     }
-
-    if (side && hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
-
-    // 6. local sort of what arrived, in place (no collective follows: a failure here is this rank's)
-    if (xp.n_recv > 0) {
-        rsort_plan p;
-        if ((st = rsort_plan_make(xp.n_recv, k_bits, pairs, 0, &p))) return st;
-        if ((st = rsort_sort_planned(&p, d_keys_out, d_vals_out, d_keys_out, d_vals_out, m.sub, m.sub_bytes, s)))
-            return st;
-    }
-    *out_n = xp.n_recv;
-    *out_offset = xp.offset;
+    if (side_pending && hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
+    *out_n = base;
+    *out_offset = xv[me * H].offset;
     return RSORT_OK;
 }
 
@@ -503,6 +542,10 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
     rsort_transport tr{&ctx, world, me, rccl_allgather, rccl_exchange};
     return multi_sort(d_keys, d_vals, n, d_keys_out, d_vals_out, capacity, out_n, out_offset, k_bits, &tr,
                       d_workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int rsort_set_multi_options(int flags) {
+    return g_multi_opts.exchange(flags & (RSORT_MULTI_OVERLAP | RSORT_MULTI_FULL));
 }
 
 int64_t rsort_set_exchange_piece(int64_t keys) {

@@ -169,6 +169,7 @@ SIGNATURES = {
     "rsort_u32_multi_transport": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int,
                                    ctypes.POINTER(Transport), _vp, _sz, _vp], _int),
     "rsort_set_exchange_piece": ([_i64], _i64),
+    "rsort_set_multi_options": ([_int], _int),
     "rsort_loopback_create": ([_int, ctypes.POINTER(ctypes.c_void_p)], _int),
     "rsort_loopback_transport": ([ctypes.c_void_p, _int, ctypes.POINTER(Transport)], _int),
     "rsort_loopback_destroy": ([ctypes.c_void_p], None),
@@ -475,6 +476,24 @@ def multi_sort_device(comm, keys, k_bits=8, vals=None, capacity=None, stream=Non
                                       _stream(stream)), "rsort_u32_multi")
     c = cnt.value
     return kout[:c], (vout[:c] if pairs else None), off.value
+
+
+MULTI_OVERLAP, MULTI_FULL = 1, 2
+
+
+def set_multi_options(flags: int) -> int:
+    """rsort_set_multi_options: MULTI_OVERLAP (sort the lower half of each rank's range while the
+    upper half is exchanged), MULTI_FULL (the whole protocol also at world 1); returns the old flags."""
+    return int(_lib().rsort_set_multi_options(int(flags)))
+
+
+@contextmanager
+def multi_options(flags: int):
+    old = set_multi_options(flags)
+    try:
+        yield
+    finally:
+        set_multi_options(old)
 
 
 def set_exchange_piece(keys: int) -> int:

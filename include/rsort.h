@@ -320,6 +320,18 @@ RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, in
                               int64_t *out_n, int64_t *out_offset, int k_bits, void *nccl_comm,
                               void *d_workspace, size_t workspace_bytes, void *stream);
 
+/* Options of rsort_u32_multi* (process-wide; returns the previous flags):
+ *  RSORT_MULTI_OVERLAP  every rank's key range is cut in two at a sampled quantile (the planning
+ *                       functions run for 2 x world ranks, world <= 8): the lower halves are
+ *                       exchanged first, and each rank sorts its lower half on a second stream
+ *                       while the upper halves are exchanged; same output. Off by default.
+ *  RSORT_MULTI_FULL     run the whole protocol also at world 1 (sample, partition into one
+ *                       bucket, self exchange): for tests and overhead measurements. By default
+ *                       one rank sorts its keys directly (the partition would be a copy). */
+#define RSORT_MULTI_OVERLAP 1
+#define RSORT_MULTI_FULL 2
+RSORT_API int rsort_set_multi_options(int flags);
+
 /* Largest message of one exchange round, in keys (default and maximum 2^28 = 1 GiB; >= 64).
  * Messages are cut into equal pieces of a multiple of 64 keys rounded DOWN, so no message exceeds
  * the limit even when it is not a multiple of 64. Process-wide; returns the previous value. Tests

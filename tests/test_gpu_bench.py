@@ -62,10 +62,11 @@ def test_bench_primitives_and_dist_path():
     d = run_bench("--primitives", "--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--configs", "")
     for k in ("copy", "histogram", "scan", "scatter", "local_sort", "partition_8"):
         assert d["primitives"][k]["ms"] > 0, k
-    for impl in ("c", "torch"):
+    for impl, extra in (("c", []), ("c", ["--dist-full"]), ("c", ["--dist-full", "--dist-overlap"]), ("torch", [])):
         d = run_bench("--dist-path", "--dist-impl", impl, "--steps", "1", "--warmup", "1", "--keys", str(1 << 24),
-                      "--no-cpu")
+                      "--no-cpu", *extra)
         assert d["value"] > 0 and "range-partition" in d["config"]["parallelism"] and d["verified"] is True
+        assert ("full protocol" in d["config"]["parallelism"]) == ("--dist-full" in extra)
 
 
 def test_bench_pairs_zipf_verified():

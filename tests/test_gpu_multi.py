@@ -96,12 +96,14 @@ def test_dist_sort_rccl_single_rank():
 
 # ------------------------------------------------------------------ C ABI: rsort_u32_multi over RCCL
 def test_c_multi_single_rank():
-    """rsort_u32_multi with a one-rank RCCL communicator: every step (top histogram, all-reduce,
-    partition, all-gather, grouped send/recv, in-place local sort) runs; result = Baseline1."""
+    """rsort_u32_multi with a one-rank RCCL communicator. With RSORT_MULTI_FULL every step (RCCL
+    all-gathers, sample sort, partition, self exchange, in-place local sort) runs; by default one
+    rank sorts directly. Result = Baseline1 either way."""
     sys.path.insert(0, str(PKG))
     import radixsort as rs
     torch.cuda.set_device(0)
     comm = rs.RcclComm(1, 0, rs.rccl_unique_id())
+    old = rs.set_multi_options(rs.MULTI_FULL)  # the whole protocol, RCCL calls included, at world 1
     try:
         for n, pairs in ((1000003, False), (600001, True), (0, False)):
             x = zipf_keys(n, seed=n) if n else np.zeros(0, np.uint32)
@@ -120,7 +122,14 @@ def test_c_multi_single_rank():
         with pytest.raises(rs.RSortError) as e:
             rs.multi_sort_device(comm, rs.from_numpy_u32(x), 8, capacity=100)
         assert e.value.status == 9
+        # default: one rank sorts directly (no partition, no self exchange), same result
+        rs.set_multi_options(0)
+        x = zipf_keys(777777, seed=3)
+        ok, _, off = rs.multi_sort_device(comm, rs.from_numpy_u32(x), 8)
+        torch.cuda.synchronize()
+        assert off == 0 and np.array_equal(rs.to_numpy_u32(ok), oracle_sort(x, 8))
     finally:
+        rs.set_multi_options(old)
         comm.close()
 
 
@@ -195,7 +204,7 @@ def _loopback_inputs(rank, n, dist_name, pairs):
     return keys, vals
 
 
-def _run_loopback(world, inputs, k, capacity=None, piece=None):
+def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0):
     """world threads in this process, one stream each, calling rsort_u32_multi_transport with
     the loopback transport on cuda:0 concurrently. Returns per-rank (keys, vals, offset) or the
     per-rank RSortError statuses."""
@@ -207,6 +216,7 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None):
         capacity = sum(int(i[0].size) for i in inputs) + 1
     grp = rs.LoopbackGroup(world)
     old_piece = rs.set_exchange_piece(piece) if piece else None
+    old_opts = rs.set_multi_options(opts)
     dev_in = [(rs.from_numpy_u32(kx), rs.from_numpy_u32(vx) if vx is not None else None) for kx, vx in inputs]
     res = [None] * world
 
@@ -229,6 +239,7 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None):
     for t in th:
         t.join(timeout=240)
     alive = any(t.is_alive() for t in th)
+    rs.set_multi_options(old_opts)
     if old_piece:
         rs.set_exchange_piece(old_piece)
     if not alive:
@@ -316,6 +327,33 @@ def test_c_multi_loopback_local_error_on_every_rank():
     assert res == [2] * world, res
 
 
+@pytest.mark.parametrize("world,dist_name,pairs,k,piece", [(2, "uniform", False, 8, None), (3, "hot", True, 8, None),
+                                                           (4, "zipf", True, 8, 5000), (4, "equal", False, 8, None),
+                                                           (5, "uniform", True, 4, None), (8, "zipf", False, 8, None),
+                                                           (3, "empty0", True, 8, None)])
+def test_c_multi_loopback_overlap(world, dist_name, pairs, k, piece):
+    """RSORT_MULTI_OVERLAP at world 2..8: the planning functions run for 2 x world ranks, each rank
+    receives its lower half first and sorts it on a side stream while its upper half is exchanged
+    (VERDICT r2 #6). Output, offsets and stability exactly as without the flag; balance within 5 %
+    where equal-key buckets exist (2 x world <= 8)."""
+    n = 200_000
+    inputs = [_loopback_inputs(r, n, dist_name, pairs) for r in range(world)]
+    res = _run_loopback(world, inputs, k, piece=piece, opts=1)
+    assert all(isinstance(x, tuple) for x in res), res
+    got = [x[0] for x in res]
+    assert [x[2] for x in res] == list(np.cumsum([0] + [g.size for g in got[:-1]]))
+    keys = np.concatenate([i[0] for i in inputs])
+    if pairs:
+        rk, rv = oracle_sort_pairs(keys, np.concatenate([i[1] for i in inputs]), k)
+        assert np.array_equal(np.concatenate(got), rk)
+        assert np.array_equal(np.concatenate([x[1] for x in res]), rv)
+    else:
+        assert np.array_equal(np.concatenate(got), oracle_sort(keys, k))
+    if 2 * world <= 8 or dist_name in ("uniform", "zipf"):
+        sizes = np.array([g.size for g in got])
+        assert np.abs(sizes - keys.size / world).max() <= 0.05 * keys.size / world + 64, sizes
+
+
 def test_c_multi_loopback_capacity_on_every_rank():
     """one rank's output too small -> EVERY rank returns RSORT_ERR_CAPACITY
     before any key moves (no rank is left waiting in the exchange)."""
@@ -356,15 +394,17 @@ def test_dist_sort_rccl_2gib_message():
 
 
 def test_c_multi_2gib_message():
-    """rsort_u32_multi over RCCL at one rank with 2^29 + 5 keys (2 GiB). The own range moves by a
-    device copy, so no RCCL message is sent: this checks the one-rank path at that size. Exchange
-    rounds are exercised by the loopback tests with small pieces (test_c_multi_loopback); a
-    multi-round RCCL exchange needs two GPUs and is unverified on the one-GPU box."""
+    """rsort_u32_multi over RCCL at one rank with 2^29 + 5 keys (2 GiB), the whole protocol
+    (RSORT_MULTI_FULL). The own range moves by a device copy, so no RCCL message is sent: this checks
+    the one-rank path at that size. Exchange rounds are exercised by the loopback tests with small
+    pieces (test_c_multi_loopback); a multi-round RCCL exchange needs two GPUs and is unverified on
+    the one-GPU box."""
     sys.path.insert(0, str(PKG))
     import radixsort as rs
     torch.cuda.set_device(0)
     n = (1 << 29) + 5
     comm = rs.RcclComm(1, 0, rs.rccl_unique_id())
+    old = rs.set_multi_options(rs.MULTI_FULL)
     try:
         keys = rs.empty_u32(n)
         rs.gen_uniform(keys, 78)
@@ -373,4 +413,5 @@ def test_c_multi_2gib_message():
         assert off == 0 and ok.numel() == n
         assert torch.equal(ok.to(torch.int64) & 0xFFFFFFFF, _sorted_ref(keys))
     finally:
+        rs.set_multi_options(old)
         comm.close()
