@@ -168,6 +168,29 @@ __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint
     return atomicAdd(&cnt[d], 1u);
 }
 
+// rank_add for input whose equal keys are contiguous: after a cut plan's pass the keys are ordered by
+// their lower digits, so from pass 2 on the copies of a key form runs (Zipf keys, passes 2 / 3: ~20 / ~5
+// runs per 64 consecutive keys) and the many medium clusters per instruction serialise in the LDS
+// whatever single digit is aggregated. Each run's first lane (a DPP wave shift finds them) adds the
+// run's length with one returning add, in lane order with other runs of the same digit; the run's
+// other lanes get that base from its first lane (ds_bpermute) + their offset in the run -- the same
+// lane-ordered rank. Instructions with more than 32 runs (pass 1: keys interleaved inside each low-digit
+// group) take rank_add_hot. All lanes must be active.
+__device__ __forceinline__ uint32_t rank_add_runs(uint32_t *cnt, uint32_t d, uint32_t &hot) {
+    const uint32_t l = lane_id();
+    // lane l - 1's digit (wave_shr:1; lane 0 gets ~d, so it always starts a run)
+    const uint32_t dp = (uint32_t)__builtin_amdgcn_update_dpp((int)~d, (int)d, 0x138, 0xF, 0xF, false);
+    const uint64_t hm = __ballot(dp != d);
+    if (__popcll(hm) > 32) return rank_add_hot(cnt, d, hot);
+    const uint64_t le = (2ull << l) - 1ull;  // lanes <= l (all ones for l = 63)
+    const uint32_t start = 63u - (uint32_t)__builtin_clzll(hm & le);
+    const uint64_t above = hm & ~le;
+    const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+    uint32_t o = 0;
+    if (start == l) o = atomicAdd(&cnt[d], next - l);
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(start << 2), (int)o) + (l - start);
+}
+
 // Row stride of per-wave digit counters [wave][digit] read column-wise by digit groups: TPD threads
 // per digit, thread `sub` taking rows sub * WPT .. + WPT - 1. With rows R apart (R a multiple of
 // 64) the TPD threads of a digit hit one bank; a stride with WPT * RS = 64 / TPD (mod 64) puts the
@@ -1471,7 +1494,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
                 const uint32_t dj = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                const uint32_t r = CL == 2 ? rank_add_runs(&s_cnt[w * RS], dj, hotd)
+                                   : CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
@@ -1849,7 +1873,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                    const uint32_t r = CL == 2 ? rank_add_runs(&s_cnt[w * RS], dj, hotd)
+                                   : CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             } else {
@@ -2178,6 +2203,16 @@ static bool pairs_lines64() {
     return v;
 }
 
+// The clustered-input kernels' ranking (CL template argument): 2 = rank_add_runs (run heads, the
+// default), 1 = rank_add_hot; RSORT_CL=1 in the environment selects the latter (A/B, dev/lab.sh).
+static int cl_ranking() {
+    static const int v = [] {
+        const char *e = getenv("RSORT_CL");
+        return (e != nullptr && e[0] == '1') ? 1 : 2;
+    }();
+    return v;
+}
+
 template <int BITS, int THREADS, int KPT, bool PAIRS, int RANK, int DMODE, int MINW>
 static void *reg_scatter() {
     void *fn = reinterpret_cast<void *>(&rs_scatter<BITS, THREADS, KPT, PAIRS, RANK, DMODE, MINW>);
@@ -2336,38 +2371,48 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
 
 // ------------------------------------------------------------------------------ lane-order probe
 // The default ranking (kRankAtomic) rests on gfx950's LDS serving the lanes of one ds_add_rtn_u32
-// that hit the same address in ascending lane order. The probe replays the production conditions
-// of rs_scatter_lines<8, 1024, 16, ...>: 1024-thread workgroups, the same per-wave rows of 256
-// counters, the SAME device function (rank_add, with its aggregated path for >= 16 equal lanes),
-// digit ranges 1..256 and runs of equal digits (the clustered input that takes the aggregated path),
-// partial exec masks -- and checks every returned rank against old value + #lower active lanes
-// with the same digit (a register-only count). Any mismatch makes the library use ballots.
-__global__ __launch_bounds__(1024) void rs_lane_order_probe(uint32_t *bad) {
+// that hit the same address in ascending lane order. The probe replays the production conditions of
+// the k = 8 line kernels: the keys shape (1024 threads, counter rows counter_stride = 260 words apart)
+// and the pairs shape (512 threads, rows 264 apart), the SAME device functions the kernels
+// instantiate -- rank_add (any exec mask), rank_add_hot with its agg_add paths and rank_add_runs
+// (full waves, as in the kernels' full tiles) -- on digit ranges 1..256, runs of equal digits (with
+// several runs sharing a digit), a run crossing the slot, partial exec masks; and checks every
+// returned rank against old value + #lower active lanes with the same digit (a register-only count).
+// Any mismatch makes the library use ballots.
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
     constexpr uint32_t R = 256;
-    constexpr int W = 1024 / kWave;
-    __shared__ uint32_t s_cnt[W * R];
+    constexpr int W = THREADS / kWave;
+    constexpr uint32_t TPD = THREADS / R;
+    constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
+    __shared__ uint32_t s_cnt[W * RS];
     const uint32_t t = threadIdx.x, w = t / kWave, lane = lane_id();
-    for (uint32_t i = t; i < W * R; i += 1024) s_cnt[i] = 0;
+    for (uint32_t i = t; i < W * RS; i += THREADS) s_cnt[i] = 0;
     __syncthreads();
     uint32_t nbad = 0;
-    for (uint32_t it = 0; it < 96; ++it) {
+    uint32_t hot = 0xFFFFFFFFu;
+    for (uint32_t it = 0; it < 192; ++it) {
         uint32_t h = (blockIdx.x * 0x9E3779B9u) ^ (it * 0x85EBCA6Bu) ^ (t * 0xC2B2AE35u);
         h ^= h >> 16;
         h *= 0x7feb352dU;
         h ^= h >> 15;
         const uint32_t hw = __builtin_amdgcn_readfirstlane((blockIdx.x * 0x27D4EB2Fu) ^ (it * 0x165667B1u) ^ w);
+        const uint32_t L = 1u + hw % 37u;  // run length of the run patterns
         uint32_t d;
-        switch (it % 6) {
+        switch (it % 8) {
             case 0: d = 0; break;                                     // one counter
             case 1: d = h % 3; break;
             case 2: d = h % 16; break;
             case 3: d = h % 256; break;                               // uniform keys
-            case 4: d = (hw + lane / (1u + hw % 37)) % 256; break;    // runs of equal digits
-            default: d = (lane < (hw % 64) ? hw : hw + 1 + (h & 1)) % 256;  // a run crossing the slot
+            case 4: d = (hw + lane / L) % 256; break;                 // runs of equal digits
+            case 5: d = (lane < (hw % 64) ? hw : hw + 1 + (h & 1)) % 256; break;  // a run crossing the slot
+            case 6: d = (hw + (lane / L) % 3) % 256; break;           // runs, several sharing a digit
+            default: d = (hw + (lane / (1u + hw % 5u)) * 7u) % 256;   // many short runs (> 32: the fallback)
         }
-        // every third iteration all lanes take part; else a hashed subset (partial exec mask)
-        const bool active = (it % 3 == 0) || ((h >> 7) % 4 != 0);
-        const uint32_t before = s_cnt[w * R + d];
+        // which ranking: rank_add (partial exec masks too), rank_add_hot, rank_add_runs (full waves)
+        const uint32_t fn = (it / 8) % 3;
+        const bool active = fn != 0 || (it % 3 == 0) || ((h >> 7) % 4 != 0);
+        const uint32_t before = s_cnt[w * RS + d];
         uint32_t below = 0;
         for (int l = 0; l < kWave; ++l) {
             const uint32_t dl = __shfl(d, l);  // every lane takes part (bpermute reads active lanes only)
@@ -2376,12 +2421,14 @@ __global__ __launch_bounds__(1024) void rs_lane_order_probe(uint32_t *bad) {
         }
         __builtin_amdgcn_wave_barrier();
         if (active) {
-            const uint32_t got = rank_add(&s_cnt[w * R], d);
+            const uint32_t got = fn == 0 ? rank_add(&s_cnt[w * RS], d)
+                               : fn == 1 ? rank_add_hot(&s_cnt[w * RS], d, hot)
+                                         : rank_add_runs(&s_cnt[w * RS], d, hot);
             nbad += got != before + below;
         }
         __builtin_amdgcn_wave_barrier();
         if (it % 24 == 23) {  // keep the counters small (each wave clears its own row)
-            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * R + i] = 0;
+            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -2401,7 +2448,8 @@ int lane_order_probe() {
     bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&bad, 4) == hipSuccess && hipMemsetAsync(bad, 0, 4, s) == hipSuccess;
     if (ok) {
-        rs_lane_order_probe<<<512, 1024, 0, s>>>(bad);
+        rs_lane_order_probe<1024><<<512, 1024, 0, s>>>(bad);  // the keys line kernels' shape
+        rs_lane_order_probe<512><<<512, 512, 0, s>>>(bad);    // the pairs kernels' shape
         ok = hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(&host, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -2463,12 +2511,15 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     // the device-side flag *cl_select picks the one that works (the other leaves at once: ~3 us)
     void *cl = nullptr;
     if (a.cl_select != nullptr) {
+        const bool runs = cl_ranking() == 2;
         if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3>))
-            cl = reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
+            cl = runs ? reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 2>()
+                      : reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
         else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2>))
-            cl = reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>();
+            cl = runs ? reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 2>()
+                      : reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>();
         else if (fn == reinterpret_cast<void *>(&rs_scatter_pairs<8, 512, 16>))
-            cl = reg_pairs<8, 512, 16, 1>();
+            cl = runs ? reg_pairs<8, 512, 16, 2>() : reg_pairs<8, 512, 16, 1>();
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass

@@ -10,6 +10,8 @@
 #   pairs            the pairs tests + C4 and Zipf keys through bench.py, then C4 with the 64-B-line
 #                    pairs kernel (RSORT_PAIRS64=1) for A/B on the same box
 #   pairslab         dev/pairs_lab: one pairs pass, 64-B vs 128-B kernels, per-phase cycles
+#   cl               the clustered-pass ranking A/B: Zipf keys and C4 through bench.py with RSORT_CL=1
+#                    (rank_add_hot) and the default (rank_add_runs)
 #   lines            dev/lines_exp: the keys line-kernel variants, uniform passes 0/1, Zipf passes 0..3
 #   zcl              dev/lines_exp "pad": clustered-kernel rank variants, uniform pass 0, Zipf passes 1, 2
 #   bench [args]     bench.py with extra args (LAB_TAG names the output)
@@ -84,6 +86,19 @@ pairslab)
         [ $rc -eq 0 ] || [ $rc -eq 3 ] || exit $rc
     done
     cat gpurun_out/pairslab.log
+    ;;
+cl)
+    for v in 2 1; do
+        RSORT_CL=$v run_bench "cl$v" --steps 2 --warmup 1 --keys 16777216 --no-cpu --no-vendor --no-e2e \
+            --configs zipf,c4 "$@" > /dev/null
+        python3 - "$v" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/cl{sys.argv[1]}.json").read().strip().splitlines()[-1])
+for k, c in d["configs"].items():
+    print("RSORT_CL=%s %-5s %8.3f ms/sort  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], k, c["ms_per_sort"],
+          c["scatter"]["avg_launch_ms"], c["scatter"]["frac"], c["verified"]))
+PY
+    done
     ;;
 lines)
     : > gpurun_out/lab_lines.log
