@@ -468,8 +468,11 @@ def main():
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     algo_bytes = bytes_per_key * keys_per_launch
     achieved = algo_bytes / (scatter_ms * 1e-3) / 1e9
-    kernel = rs.scatter_kernel_name(p) if not use_dist else "rs_scatter_lines (partition and sort passes)"
-    cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel}"
+    # the pass's working kernel: the plain variant (the clustered-input twins end in ", 1>" / ", 2>")
+    plain = [k for k in kernels_used if not (k.endswith(", 1>") or k.endswith(", 2>")) or k.startswith("rs_scatter<")]
+    kernel = (plain[-1] if plain else rs.scatter_kernel_name(p)) if not use_dist else \
+        "rs_scatter_lines (partition and sort passes)"
+    cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel.split('<')[0]}"
     prec, prec_src = profile_record(cfg_key) if not use_dist else (None, None)
 
     vendor = None
@@ -515,9 +518,6 @@ def main():
 
     if rank == 0:
         total_keys = n * world * a.steps
-        plain = [k for k in kernels_used if not k.endswith(", 1>")]  # (", 1>": the clustered-input variant)
-        if plain and not use_dist:
-            kernel = plain[-1]
         roof = {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -349,7 +349,7 @@ def test_c_multi_loopback_overlap(world, dist_name, pairs, k, piece):
         assert np.array_equal(np.concatenate([x[1] for x in res]), rv)
     else:
         assert np.array_equal(np.concatenate(got), oracle_sort(keys, k))
-    if 2 * world <= 8 or dist_name in ("uniform", "zipf"):
+    if 2 * world <= 8 or dist_name == "uniform":  # (above 8 virtual ranks: no equal-key buckets)
         sizes = np.array([g.size for g in got])
         assert np.abs(sizes - keys.size / world).max() <= 0.05 * keys.size / world + 64, sizes
 
