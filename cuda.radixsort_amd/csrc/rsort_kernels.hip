@@ -1737,7 +1737,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 // chunk's output) and ends with masked dword stores of the carries (both lines are shared with the
 // neighbouring chunks). Digit-group chunks (a.bounds) and the clustered-input ranking (CL) as in
 // rs_scatter_lines.
-template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1>
+// (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
+// the next tile's loads issued before the rank loop instead of after it)
+template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -1807,8 +1809,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
         if (valid == T) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                k[j] = tk[j * kWave];
-                v[j] = tv[j * kWave];
+                k[j] = (OPT & 1) ? __builtin_nontemporal_load(tk + j * kWave) : tk[j * kWave];
+                v[j] = (OPT & 1) ? __builtin_nontemporal_load(tv + j * kWave) : tv[j * kWave];
             }
         } else {
             const uint32_t lim = valid > lb ? valid - lb : 0u;
@@ -1869,6 +1871,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
             uint32_t rk[(KPT + 1) / 2];
             uint32_t nkey[PF == 1 ? KPT : 1], nval[PF == 1 ? KPT : 1];
+            if constexpr (PF == 1 && (OPT & 2)) {
+                if (nb < cend) load_tile(nb, nkey, nval);
+            }
             if (full) {
     #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
@@ -1886,7 +1891,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
-            if constexpr (PF == 1) {
+            if constexpr (PF == 1 && !(OPT & 2)) {
                 if (nb < cend) load_tile(nb, nkey, nval);
             }
             // (the previous tile's step 4 has read the bitmap: behind the barrier below)

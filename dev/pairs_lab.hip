@@ -196,6 +196,15 @@ int main(int argc, char **argv) {
         printf("  1024 x 8 outputs equal: %s\n", e1 && memcmp(x.data(), y.data(), n * 4) == 0 ? "yes" : "NO");
     }
     timeit("rs_scatter_pairs 1024 x 8, CL", [&] { rs_scatter_pairs<8, 1024, 8, 1><<<chunks, 1024>>>(sb); });
+    timeit("rs_scatter_pairs 1024 x 8, CL runs", [&] { rs_scatter_pairs<8, 1024, 8, 2><<<chunks, 1024>>>(sb); });
+    timeit("rs_scatter_pairs 512 x 16, CL runs", [&] { rs_scatter_pairs<8, 512, 16, 2><<<chunks, 512>>>(sb); });
+    timeit("rs_scatter_lines pairs (64-B), CL runs", [&] {
+        rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 2><<<chunks, 512>>>(args(in_k, in_v, ka, va, shift));
+    });
+    timeit("rs_scatter_pairs nt loads", [&] { rs_scatter_pairs<8, 512, 16, 0, 1, 1><<<chunks, 512>>>(sb); });
+    timeit("rs_scatter_pairs early loads", [&] { rs_scatter_pairs<8, 512, 16, 0, 1, 2><<<chunks, 512>>>(sb); });
+    timeit("rs_scatter_pairs 1024 x 8 nt loads", [&] { rs_scatter_pairs<8, 1024, 8, 0, 1, 1><<<chunks, 1024>>>(sb); });
+    timeit("rs_scatter_pairs 1024 x 8 early loads", [&] { rs_scatter_pairs<8, 1024, 8, 0, 1, 2><<<chunks, 1024>>>(sb); });
     const char *ph[] = {"rank+load wait", "segments+carry", "line records", "staging", "output", "", "", ""};
     printf("  rs_scatter_pairs cycles per tile (thread 0, mean over chunks):");
     for (int i = 0; i < 5; ++i) {
