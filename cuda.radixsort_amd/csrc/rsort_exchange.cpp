@@ -179,4 +179,18 @@ int rsort_multi_exchange_plan(int world, int me, int buckets, const int64_t *cou
     return out->over_capacity >= 0 ? RSORT_ERR_CAPACITY : RSORT_OK;
 }
 
+int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, int64_t *rounds, int64_t *piece) {
+    if (!rounds || !piece || max_message < 0 || limit < 1) return RSORT_ERR_ARG;
+    *rounds = 0;
+    *piece = 0;
+    if (max_message == 0) return RSORT_OK;
+    limit = std::max<int64_t>(limit, 64);
+    const int64_t r0 = (max_message + limit - 1) / limit;  // rounds at the limit
+    int64_t p = (max_message + r0 - 1) / r0;               // equal pieces, <= limit
+    p = std::max<int64_t>(64, p / 64 * 64);                // a multiple of 64, rounded down
+    *piece = p;
+    *rounds = (max_message + p - 1) / p;
+    return RSORT_OK;
+}
+
 }  // extern "C"

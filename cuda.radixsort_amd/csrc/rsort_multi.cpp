@@ -273,21 +273,6 @@ int d2h(void *h, const void *d, size_t bytes, hipStream_t s) {
     return hip_st(hipStreamSynchronize(s));
 }
 
-// Exchange rounds for messages of up to max_message keys with at most `limit` keys per message:
-// equal pieces, a multiple of 64 keys (256-B aligned message starts) and never above the limit
-// (rounded down, so a limit that is not a multiple of 64 still holds).
-void exchange_rounds(int64_t max_message, int64_t limit, int64_t *rounds, int64_t *piece) {
-    *rounds = 0;
-    *piece = 0;
-    if (max_message <= 0) return;
-    limit = std::max<int64_t>(limit, 64);
-    const int64_t r0 = (max_message + limit - 1) / limit;      // rounds at the limit
-    int64_t p = (max_message + r0 - 1) / r0;                    // equal pieces, <= limit
-    p = std::max<int64_t>(64, p / 64 * 64);
-    *piece = p;
-    *rounds = (max_message + p - 1) / p;
-}
-
 int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32_t *d_keys_out, uint32_t *d_vals_out,
                int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits, const rsort_transport *tr,
                void *d_workspace, size_t workspace_bytes, hipStream_t s) {
@@ -440,7 +425,7 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     //      limit), then the local sort of what arrived, in place. With two halves the first half's
     //      sort runs on the side stream while the second half is exchanged.
     int64_t rounds = 0, piece = 0;
-    exchange_rounds(xs.max_message, g_piece.load(), &rounds, &piece);
+    if ((st = rsort_multi_exchange_rounds(xs.max_message, g_piece.load(), &rounds, &piece))) return st;
     SideStream *side = side_stream();
     struct SideGuard {
         SideStream *x;

@@ -80,14 +80,9 @@ class GpuOps:
 
 
 def exchange_rounds(max_message: int, limit: int) -> tuple[int, int]:
-    """(rounds, piece) for messages of up to max_message keys, <= limit keys each: equal pieces
-    of a multiple of 64 keys, rounded down (rsort_multi.cpp exchange_rounds)."""
-    if max_message <= 0:
-        return 0, 0
-    limit = max(limit, 64)
-    r0 = -(-max_message // limit)
-    piece = max(64, (-(-max_message // r0)) // 64 * 64)
-    return -(-max_message // piece), piece
+    """(rounds, piece) for messages of up to max_message keys, <= limit keys each: the C planning
+    function rsort_multi_exchange_rounds (pieces a multiple of 64 keys, rounded down)."""
+    return rs.multi_exchange_rounds(max_message, limit)
 
 
 def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, capacity=None):

@@ -170,6 +170,7 @@ SIGNATURES = {
                                    ctypes.POINTER(Transport), _vp, _sz, _vp], _int),
     "rsort_set_exchange_piece": ([_i64], _i64),
     "rsort_set_multi_options": ([_int], _int),
+    "rsort_multi_exchange_rounds": ([_i64, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
     "rsort_loopback_create": ([_int, ctypes.POINTER(ctypes.c_void_p)], _int),
     "rsort_loopback_transport": ([ctypes.c_void_p, _int, ctypes.POINTER(Transport)], _int),
     "rsort_loopback_destroy": ([ctypes.c_void_p], None),
@@ -536,6 +537,15 @@ def sample_device(keys, stride: int, count: int, row_len: int, out=None, stream=
     _check(_lib().rsort_sample_device(_ptr(keys), keys.numel(), int(stride), int(count), int(row_len), _ptr(out),
                                       _stream(stream)), "rsort_sample_device")
     return out
+
+
+def multi_exchange_rounds(max_message: int, limit: int) -> tuple[int, int]:
+    """rsort_multi_exchange_rounds: (rounds, piece) of the exchange for messages of up to max_message
+    keys, at most `limit` keys each."""
+    r, p = ctypes.c_int64(), ctypes.c_int64()
+    _check(_lib().rsort_multi_exchange_rounds(int(max_message), int(limit), ctypes.byref(r), ctypes.byref(p)),
+           "rsort_multi_exchange_rounds")
+    return int(r.value), int(p.value)
 
 
 def multi_quantile_index(sp: SamplePlan, i: int) -> int:

@@ -290,6 +290,11 @@ RSORT_API int rsort_multi_exchange_plan(int world, int me, int buckets, const in
                                         const rsort_multi_splitters *sp, const int64_t *capacity,
                                         rsort_exchange_plan *out);
 
+/* 4. Exchange rounds. Messages of up to max_message keys (the plan's max_message), at most `limit`
+ * keys each: *rounds equal pieces of *piece keys, a multiple of 64 keys rounded DOWN (never above
+ * the limit; >= 64), rounds * piece >= max_message. (0, 0) for max_message 0. */
+RSORT_API int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, int64_t *rounds, int64_t *piece);
+
 /* ---------------------------------------------------------------- multi-GPU sort */
 /* One rank per GPU (the reference is single-GPU, Parallel7.cu:10). Every rank
  * passes its n local keys (and values); on return rank r's d_keys_out[0 .. *out_n) holds the keys

@@ -36,6 +36,16 @@ static uint64_t next() {
 
 int main(int argc, char **argv) {
     const int cases = argc > 1 ? atoi(argv[1]) : 20000;
+    // exchange rounds: pieces never above the limit, a multiple of 64, covering the message
+    for (int c = 0; c < cases; ++c) {
+        const int64_t m = (int64_t)(next() % ((uint64_t)1 << (next() % 41)));
+        const int64_t limit = 1 + (int64_t)(next() % ((uint64_t)1 << (1 + next() % 30)));
+        int64_t r = -1, p = -1;
+        if (rsort_multi_exchange_rounds(m, limit, &r, &p) != RSORT_OK) FAIL("exchange_rounds failed");
+        if (m == 0 && (r != 0 || p != 0)) FAIL("rounds of an empty message");
+        if (m > 0 && (p < 64 || p % 64 != 0 || p > std::max<int64_t>(limit, 64) || r * p < m || (r - 1) * p >= m))
+            FAIL("rounds m=%lld limit=%lld -> %lld x %lld", (long long)m, (long long)limit, (long long)r, (long long)p);
+    }
     for (int c = 0; c < cases; ++c) {
         const int world = 1 + (int)(next() % RSORT_MAX_RANKS);
         // quantile keys: sorted, with repeats and the extreme keys
