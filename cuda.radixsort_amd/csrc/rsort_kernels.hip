@@ -1738,7 +1738,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 // neighbouring chunks). Digit-group chunks (a.bounds) and the clustered-input ranking (CL) as in
 // rs_scatter_lines.
 // (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
-// the next tile's loads issued before the rank loop instead of after it)
+// the next tile's loads issued before the rank loop instead of after it, OPT & 4 keys and values
+// staged interleaved)
 template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
@@ -1757,8 +1758,11 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     static_assert(CAP + 40 < 65536u && NLM < 65536u, "slot and line indices packed in 16 bits");
 
     // [0, CAP) segments; [CAP, CAP + 32) the last tail read's overrun; CAP + 32 the padding sink
-    __shared__ __attribute__((aligned(16))) uint32_t s_k[CAP + 36];
-    __shared__ __attribute__((aligned(16))) uint32_t s_v[CAP + 36];
+    // OPT & 4: one interleaved {key, value} array (8-B stores per pair) instead of two
+    constexpr bool IL = (OPT & 4) != 0;
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[IL ? 4 : CAP + 36];
+    __shared__ __attribute__((aligned(16))) uint32_t s_v[IL ? 4 : CAP + 36];
+    __shared__ __attribute__((aligned(16))) uint2 s_kv[IL ? CAP + 36 : 2];
     constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
     __shared__ uint32_t s_cnt[W * RS + 1];
     __shared__ uint4 s_rec[R];        // per digit: {global - 32 x first line, LDS - 32 x first line, first line << 8 | inv}
@@ -1834,8 +1838,16 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
         const uint32_t V = item / QPL, q = (item % QPL) * 4u;
         const uint2 lr = s_lrec[V];
         const uint32_t li = (lr.y & 0xFFFFu) + q;
-        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_k[li]);
-        const u32x4 vv = *reinterpret_cast<const u32x4 *>(&s_v[li]);
+        u32x4 kv, vv;
+        if constexpr (IL) {
+            const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[li]);
+            const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[li + 2]);
+            kv = u32x4{p01.x, p01.z, p23.x, p23.z};
+            vv = u32x4{p01.y, p01.w, p23.y, p23.w};
+        } else {
+            kv = *reinterpret_cast<const u32x4 *>(&s_k[li]);
+            vv = *reinterpret_cast<const u32x4 *>(&s_v[li]);
+        }
         const uint64_t gp = (uint64_t)(lr.x + q);
         const uint32_t lo = lr.y >> 16;
         if (lo <= q) {
@@ -1936,8 +1948,14 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     #pragma unroll
             for (uint32_t i = 0; i < CPT; i += 4) {
                 if (sub * CPT + i < carry) {
-                    *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
-                    *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+                    if constexpr (IL) {
+                        *reinterpret_cast<u32x4 *>(&s_kv[S + sub * CPT + i]) = u32x4{ck[i], cv[i], ck[i + 1], cv[i + 1]};
+                        *reinterpret_cast<u32x4 *>(&s_kv[S + sub * CPT + i + 2]) =
+                            u32x4{ck[i + 2], cv[i + 2], ck[i + 3], cv[i + 3]};
+                    } else {
+                        *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
+                        *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+                    }
                 }
             }
             if (leader) {
@@ -1976,8 +1994,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     const int j = j0 + u;
                     uint32_t idx = pp[u];
                     if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
-                    s_k[idx] = key[j];
-                    s_v[idx] = val[j];
+                    if constexpr (IL) {
+                        s_kv[idx] = make_uint2(key[j], val[j]);
+                    } else {
+                        s_k[idx] = key[j];
+                        s_v[idx] = val[j];
+                    }
                 }
             }
             // PF = 2: this tile's registers are free (staged): the tile after next goes into them, in
@@ -1995,8 +2017,16 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     #pragma unroll
                 for (uint32_t i = 0; i < CPT; i += 4) {
                     if (sub * CPT + i >= ncarry) break;
-                    const u32x4 kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
-                    const u32x4 vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
+                    u32x4 kq, vq;
+                    if constexpr (IL) {
+                        const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i]);
+                        const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i + 2]);
+                        kq = u32x4{p01.x, p01.z, p23.x, p23.z};
+                        vq = u32x4{p01.y, p01.w, p23.y, p23.w};
+                    } else {
+                        kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+                        vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
+                    }
                     ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
                     cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
                 }

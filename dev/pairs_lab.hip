@@ -201,6 +201,17 @@ int main(int argc, char **argv) {
     timeit("rs_scatter_lines pairs (64-B), CL runs", [&] {
         rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 2><<<chunks, 512>>>(args(in_k, in_v, ka, va, shift));
     });
+    timeit("rs_scatter_pairs interleaved staging", [&] { rs_scatter_pairs<8, 512, 16, 0, 1, 4><<<chunks, 512>>>(sb); });
+    {
+        std::vector<uint32_t> x(n), y(n);
+        CK(hipMemcpy(x.data(), ka, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), kb, n * 4, hipMemcpyDeviceToHost));
+        const bool e1 = memcmp(x.data(), y.data(), n * 4) == 0;
+        CK(hipMemcpy(x.data(), va, n * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y.data(), vb, n * 4, hipMemcpyDeviceToHost));
+        printf("  interleaved outputs equal: %s\n", e1 && memcmp(x.data(), y.data(), n * 4) == 0 ? "yes" : "NO");
+    }
+    timeit("rs_scatter_pairs 1024 x 8 interleaved", [&] { rs_scatter_pairs<8, 1024, 8, 0, 1, 4><<<chunks, 1024>>>(sb); });
     timeit("rs_scatter_pairs nt loads", [&] { rs_scatter_pairs<8, 512, 16, 0, 1, 1><<<chunks, 512>>>(sb); });
     timeit("rs_scatter_pairs early loads", [&] { rs_scatter_pairs<8, 512, 16, 0, 1, 2><<<chunks, 512>>>(sb); });
     timeit("rs_scatter_pairs 1024 x 8 nt loads", [&] { rs_scatter_pairs<8, 1024, 8, 0, 1, 1><<<chunks, 1024>>>(sb); });
