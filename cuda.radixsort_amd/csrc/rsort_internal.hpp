@@ -23,7 +23,8 @@ enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 // 4096-key tiles (LDS for 2^k per-wave counters; enough workgroups to fill 256 CUs).
 // kGeomLines (k = 5..8 keys): 16384-key tiles of 1024 threads written as whole 128-B lines
 // (rs_scatter_lines; one workgroup per CU, its LDS holds the tile plus every digit's carry).
-// kGeomLinesPairs (k = 5..8 pairs): 8192-key tiles of 512 threads (keys + values), 64-B lines.
+// kGeomLinesPairs (k = 5..8 pairs): 8192-pair tiles of 1024 threads x 8 (keys + values); k = 7, 8
+// through rs_scatter_pairs (128-B lines in both arrays), k = 5, 6 through rs_scatter_lines (64-B lines).
 // kGeomXL (k = 13): 4096-key tiles of 128 threads (2 waves), so the 2 x 8192 per-wave counters fit
 // in LDS beside the tile (112 KB keys-only).
 enum Geom : int { kGeomSmall = 0, kGeomLarge = 1, kGeomK4 = 2, kGeomLines = 3, kGeomLinesPairs = 4, kGeomXL = 5,
@@ -32,20 +33,18 @@ struct GeomShape {
     int threads;
     int kpt;
 };
-constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {512, 16}, {128, 32}};
+constexpr GeomShape kGeomShape[kGeomCount] = {{256, 16}, {512, 32}, {512, 16}, {1024, 16}, {1024, 8}, {128, 32}};
 // rs_scatter_lines line width. Keys-only stages whole 128-B lines (the L2 line: runs that start or
-// end mid-line cost about a third more HBM time, dev/runlen_lab.hip); pairs keep 64-B lines (two
-// 128-B carry areas do not fit in LDS beside 8192-key tiles of keys and values).
+// end mid-line cost about a third more HBM time, dev/runlen_lab.hip); its pairs instances keep 64-B
+// lines (two 128-B carry areas do not fit in LDS beside 8192-key tiles of keys and values) --
+// rs_scatter_pairs writes 128-B lines for pairs with its own layout.
 constexpr int kLineKeys = 32;
 constexpr int kLineKeysPairs = 16;
 inline int geom_tile_keys(int g) { return kGeomShape[g].threads * kGeomShape[g].kpt; }
-// K4 and LinesPairs share a shape; pairs (K4 is keys-only) tell them apart.
 inline int geom_from_shape(int threads, int tile_keys, int pairs) {
+    (void)pairs;
     for (int g = 0; g < kGeomCount; ++g)
-        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) {
-            if (g == kGeomK4 && pairs) return kGeomLinesPairs;
-            return g;
-        }
+        if (kGeomShape[g].threads == threads && geom_tile_keys(g) == tile_keys) return g;
     return -1;
 }
 

@@ -168,29 +168,6 @@ __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint
     return atomicAdd(&cnt[d], 1u);
 }
 
-// rank_add for input whose equal keys are contiguous: after a cut plan's pass the keys are ordered by
-// their lower digits, so from pass 2 on the copies of a key form runs (Zipf keys, passes 2 / 3: ~20 / ~5
-// runs per 64 consecutive keys) and the many medium clusters per instruction serialise in the LDS
-// whatever single digit is aggregated. Each run's first lane (a DPP wave shift finds them) adds the
-// run's length with one returning add, in lane order with other runs of the same digit; the run's
-// other lanes get that base from its first lane (ds_bpermute) + their offset in the run -- the same
-// lane-ordered rank. Instructions with more than 32 runs (pass 1: keys interleaved inside each low-digit
-// group) take rank_add_hot. All lanes must be active.
-__device__ __forceinline__ uint32_t rank_add_runs(uint32_t *cnt, uint32_t d, uint32_t &hot) {
-    const uint32_t l = lane_id();
-    // lane l - 1's digit (wave_shr:1; lane 0 gets ~d, so it always starts a run)
-    const uint32_t dp = (uint32_t)__builtin_amdgcn_update_dpp((int)~d, (int)d, 0x138, 0xF, 0xF, false);
-    const uint64_t hm = __ballot(dp != d);
-    if (__popcll(hm) > 32) return rank_add_hot(cnt, d, hot);
-    const uint64_t le = (2ull << l) - 1ull;  // lanes <= l (all ones for l = 63)
-    const uint32_t start = 63u - (uint32_t)__builtin_clzll(hm & le);
-    const uint64_t above = hm & ~le;
-    const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : 64u;
-    uint32_t o = 0;
-    if (start == l) o = atomicAdd(&cnt[d], next - l);
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(start << 2), (int)o) + (l - start);
-}
-
 // Row stride of per-wave digit counters [wave][digit] read column-wise by digit groups: TPD threads
 // per digit, thread `sub` taking rows sub * WPT .. + WPT - 1. With rows R apart (R a multiple of
 // 64) the TPD threads of a digit hit one bank; a stride with WPT * RS = 64 / TPD (mod 64) puts the
@@ -1413,11 +1390,12 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         const uint64_t gp = (uint64_t)(info.x + L * G + q);
         if constexpr (NX) {
             if (count_next) {
-                // a quad never straddles a chunk boundary (both are multiples of 4 keys)
-                const uint32_t slot = (uint32_t)gp - a.pos_shift >= s_nb[d] ? 1u : 0u;
+                // (per element: with a pos_shift that is not a multiple of 4 a quad can straddle a
+                // chunk boundary of the unshifted positions)
+                const uint32_t p0 = (uint32_t)gp - a.pos_shift;
 #pragma unroll
                 for (uint32_t x = 0; x < 4; ++x)
-                    if (lo <= q + x) next_add(d, slot, kv[x]);
+                    if (lo <= q + x) next_add(d, p0 + x >= s_nb[d] ? 1u : 0u, kv[x]);
             }
         }
         if (lo <= q) {
@@ -1494,8 +1472,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
                 // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
                 const uint32_t dj = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                const uint32_t r = CL == 2 ? rank_add_runs(&s_cnt[w * RS], dj, hotd)
-                                   : CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
@@ -1890,8 +1867,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
-                    const uint32_t r = CL == 2 ? rank_add_runs(&s_cnt[w * RS], dj, hotd)
-                                   : CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                    const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             } else {
@@ -2228,22 +2204,12 @@ static void *reg_pairs() {
     return fn;
 }
 
-// Pairs with k = 6..8 write 128-B lines through rs_scatter_pairs; RSORT_PAIRS64=1 in the environment
+// Pairs with k = 7, 8 write 128-B lines through rs_scatter_pairs; RSORT_PAIRS64=1 in the environment
 // selects rs_scatter_lines' 64-B-line pairs kernel instead (A/B measurements, dev/lab.sh).
 static bool pairs_lines64() {
     static const bool v = [] {
         const char *e = getenv("RSORT_PAIRS64");
         return e != nullptr && e[0] != '\0' && e[0] != '0';
-    }();
-    return v;
-}
-
-// The clustered-input kernels' ranking (CL template argument): 2 = rank_add_runs (run heads, the
-// default), 1 = rank_add_hot; RSORT_CL=1 in the environment selects the latter (A/B, dev/lab.sh).
-static int cl_ranking() {
-    static const int v = [] {
-        const char *e = getenv("RSORT_CL");
-        return (e != nullptr && e[0] == '1') ? 1 : 2;
     }();
     return v;
 }
@@ -2350,7 +2316,7 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         // only (dev/scatter_lab LAB_PAIRS, 2^30: 4.24 -> 3.96 ms; nt loads 4.66 ms)
         constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
         if (geom == GL) {
-            if constexpr (PAIRS && BITS >= 6) {
+            if constexpr (PAIRS && (kGeomShape[GL].threads >> BITS) <= 8) {  // (carry slots per thread >= 4)
                 if (rank == kRankAtomic && aligned16 && !pairs_lines64())
                     return reg_pairs<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt>();
             }
@@ -2407,11 +2373,12 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
 // ------------------------------------------------------------------------------ lane-order probe
 // The default ranking (kRankAtomic) rests on gfx950's LDS serving the lanes of one ds_add_rtn_u32
 // that hit the same address in ascending lane order. The probe replays the production conditions of
-// the k = 8 line kernels: the keys shape (1024 threads, counter rows counter_stride = 260 words apart)
-// and the pairs shape (512 threads, rows 264 apart), the SAME device functions the kernels
-// instantiate -- rank_add (any exec mask), rank_add_hot with its agg_add paths and rank_add_runs
-// (full waves, as in the kernels' full tiles) -- on digit ranges 1..256, runs of equal digits (with
-// several runs sharing a digit), a run crossing the slot, partial exec masks; and checks every
+// the line kernels: the 1024-thread shape of the k = 8 keys and pairs kernels (counter rows
+// counter_stride = 260 words apart) and the 512-thread shape of the partition kernels (rows 264
+// apart at 256 digits), the SAME device functions the kernels
+// instantiate -- rank_add (any exec mask) and rank_add_hot with its agg_add paths (full waves, as in
+// the kernels' full tiles) -- on digit ranges 1..256, runs of equal digits (with several runs sharing
+// a digit), a run crossing the slot, partial exec masks; and checks every
 // returned rank against old value + #lower active lanes with the same digit (a register-only count).
 // Any mismatch makes the library use ballots.
 template <int THREADS>
@@ -2444,8 +2411,8 @@ __global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
             case 6: d = (hw + (lane / L) % 3) % 256; break;           // runs, several sharing a digit
             default: d = (hw + (lane / (1u + hw % 5u)) * 7u) % 256;   // many short runs (> 32: the fallback)
         }
-        // which ranking: rank_add (partial exec masks too), rank_add_hot, rank_add_runs (full waves)
-        const uint32_t fn = (it / 8) % 3;
+        // which ranking: rank_add (partial exec masks too), rank_add_hot (full waves, as in the kernels)
+        const uint32_t fn = (it / 8) % 2;
         const bool active = fn != 0 || (it % 3 == 0) || ((h >> 7) % 4 != 0);
         const uint32_t before = s_cnt[w * RS + d];
         uint32_t below = 0;
@@ -2456,9 +2423,7 @@ __global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
         }
         __builtin_amdgcn_wave_barrier();
         if (active) {
-            const uint32_t got = fn == 0 ? rank_add(&s_cnt[w * RS], d)
-                               : fn == 1 ? rank_add_hot(&s_cnt[w * RS], d, hot)
-                                         : rank_add_runs(&s_cnt[w * RS], d, hot);
+            const uint32_t got = fn == 0 ? rank_add(&s_cnt[w * RS], d) : rank_add_hot(&s_cnt[w * RS], d, hot);
             nbad += got != before + below;
         }
         __builtin_amdgcn_wave_barrier();
@@ -2483,8 +2448,8 @@ int lane_order_probe() {
     bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
               hipMalloc(&bad, 4) == hipSuccess && hipMemsetAsync(bad, 0, 4, s) == hipSuccess;
     if (ok) {
-        rs_lane_order_probe<1024><<<512, 1024, 0, s>>>(bad);  // the keys line kernels' shape
-        rs_lane_order_probe<512><<<512, 512, 0, s>>>(bad);    // the pairs kernels' shape
+        rs_lane_order_probe<1024><<<512, 1024, 0, s>>>(bad);  // the k = 8 keys and pairs kernels' shape
+        rs_lane_order_probe<512><<<512, 512, 0, s>>>(bad);    // 512-thread workgroups (partitions)
         ok = hipGetLastError() == hipSuccess &&
              hipMemcpyAsync(&host, bad, 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
              hipStreamSynchronize(s) == hipSuccess;
@@ -2546,15 +2511,13 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     // the device-side flag *cl_select picks the one that works (the other leaves at once: ~3 us)
     void *cl = nullptr;
     if (a.cl_select != nullptr) {
-        const bool runs = cl_ranking() == 2;
+        constexpr int PT = kGeomShape[kGeomLinesPairs].threads, PK = kGeomShape[kGeomLinesPairs].kpt;
         if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3>))
-            cl = runs ? reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 2>()
-                      : reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
-        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2>))
-            cl = runs ? reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 2>()
-                      : reg_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1>();
-        else if (fn == reinterpret_cast<void *>(&rs_scatter_pairs<8, 512, 16>))
-            cl = runs ? reg_pairs<8, 512, 16, 2>() : reg_pairs<8, 512, 16, 1>();
+            cl = reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, PT, PK, kLineKeysPairs, true, kDigitShift, 2>))
+            cl = reg_lines<8, PT, PK, kLineKeysPairs, true, kDigitShift, 2, 1>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_pairs<8, PT, PK>))
+            cl = reg_pairs<8, PT, PK, 1>();
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass

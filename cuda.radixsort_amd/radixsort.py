@@ -393,12 +393,13 @@ def get_group_chunks() -> bool:
 
 
 def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
-    """Which scatter kernel a sort with plan `p` runs (mirrors the dispatch in rsort_kernels.hip)."""
+    """Which scatter kernel family a sort with plan `p` runs (a mirror of the dispatch in
+    rsort_kernels.hip; scatter_kernels_used() reports what actually ran)."""
     lines = ((p.threads, p.tile_keys) == (1024, 16384) and not p.pairs) or \
-        ((p.threads, p.tile_keys) == (512, 8192) and p.pairs and 5 <= p.k_bits <= 8) or \
+        ((p.threads, p.tile_keys) == (1024, 8192) and p.pairs and 5 <= p.k_bits <= 8) or \
         ((p.threads, p.tile_keys) == (256, 4096) and not p.pairs and 3 <= p.k_bits <= 4)
     if lines and out_aligned16 and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
-        return "rs_scatter_lines"
+        return "rs_scatter_pairs" if p.pairs and p.k_bits >= 7 else "rs_scatter_lines"
     return "rs_scatter"
 
 

@@ -49,7 +49,7 @@ def test_plan_geometry(n, k):
     assert (p.threads, p.tile_keys) in {(256, 4096), (512, 16384), (512, 8192), (1024, 16384)}
     if n >= 2 * 256 * 16384 and 5 <= k <= 8:
         assert (p.threads, p.tile_keys) == (1024, 16384)  # whole-line (rs_scatter_lines) tiles
-        assert (rs.plan(n, k, True).threads, rs.plan(n, k, True).tile_keys) == (512, 8192)  # pairs lines
+        assert (rs.plan(n, k, True).threads, rs.plan(n, k, True).tile_keys) == (1024, 8192)  # pairs lines
     assert p.chunk_keys == p.tiles_per_chunk * p.tile_keys
     assert p.num_chunks * p.chunk_keys >= n
     assert (p.num_chunks - 1) * p.chunk_keys < max(n, 1)

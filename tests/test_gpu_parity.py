@@ -188,8 +188,10 @@ def test_pairs_values_misaligned_against_keys_falls_back():
         rs.sort_device(dev(x), out, 8, vals_in=dev(vals), vals_out=vout)
         torch.cuda.synchronize()
         assert np.array_equal(host(out), rk) and np.array_equal(host(vout), rv), (ko, vo)
+        # (the passes into the workspace's ping-pong buffers take the line kernels either way; the
+        # passes into the caller's buffers take rs_scatter when their offsets disagree)
         used = rs.scatter_kernels_used(reset=True)
-        assert any(u.startswith("rs_scatter_pairs") or u.startswith("rs_scatter_lines") for u in used) == lines, used
+        assert any(u.startswith("rs_scatter<") for u in used) == (not lines), used
 
 
 def test_whole_line_scatter_16b_aligned_output():
