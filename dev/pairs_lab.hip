@@ -148,12 +148,8 @@ int main(int argc, char **argv) {
     std::vector<Var> vars = {
         {"rs_scatter_lines 64-B 512 x 16", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2><<<g, 512>>>(x); }, 1e9f, {}},
-        {"rs_scatter_lines 64-B 512 x 16, CL", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2, 1><<<g, 512>>>(x); }, 1e9f, {}},
         {"rs_scatter_lines 64-B 1024 x 8", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_lines<8, 1024, 8, kLineKeysPairs, true, kDigitShift, 2><<<g, 1024>>>(x); }, 1e9f, {}},
-        {"rs_scatter_pairs 128-B 512 x 16", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_pairs<8, 512, 16><<<g, 512>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_pairs<8, 1024, 8><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8, CL", [](const ScatterArgs &x, uint32_t g) {
@@ -162,6 +158,14 @@ int main(int argc, char **argv) {
              rs_scatter_pairs<8, 1024, 8, 0, 1, 1><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8, interleaved", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_pairs<8, 1024, 8, 0, 1, 4><<<g, 1024>>>(x); }, 1e9f, {}},
+        {"rs_scatter_pairs 128-B 1024 x 8, CL interleaved", [](const ScatterArgs &x, uint32_t g) {
+             rs_scatter_pairs<8, 1024, 8, 1, 1, 4><<<g, 1024>>>(x); }, 1e9f, {}},
+        {"rs_scatter_pairs 128-B 1024 x 8, CL nt loads", [](const ScatterArgs &x, uint32_t g) {
+             rs_scatter_pairs<8, 1024, 8, 1, 1, 1><<<g, 1024>>>(x); }, 1e9f, {}},
+        {"rs_scatter_pairs 128-B 1024 x 8, CL interleaved nt", [](const ScatterArgs &x, uint32_t g) {
+             rs_scatter_pairs<8, 1024, 8, 1, 1, 5><<<g, 1024>>>(x); }, 1e9f, {}},
+        {"rs_scatter_pairs 128-B 1024 x 8, CL early loads", [](const ScatterArgs &x, uint32_t g) {
+             rs_scatter_pairs<8, 1024, 8, 1, 1, 2><<<g, 1024>>>(x); }, 1e9f, {}},
     };
     const int rounds = env_int("PL_ROUNDS", 3);
     std::vector<uint32_t> refk(n), refv(n), gk(n), gv(n);

@@ -238,6 +238,27 @@ def test_pairs_stable_vs_oracle(k, algo):
         assert np.array_equal(host(ov), vo_ref)
 
 
+@pytest.mark.parametrize("k", [5, 6, 7, 8])
+@pytest.mark.parametrize("dist_name", ["uniform", "zipf"])
+def test_pairs_line_tiles_vs_oracle(k, dist_name):
+    """Pairs large enough for the 1024 x 8 pair tiles (kGeomLinesPairs): k = 7, 8 through
+    rs_scatter_pairs (128-B lines in both arrays, register carries), k = 5, 6 through the 64-B-line
+    rs_scatter_lines instances; ragged n, bit-exact against the oracle's stable pairs sort."""
+    n = (1 << 23) + 4321
+    keys = zipf_keys(n, seed=k) if dist_name == "zipf" else uniform_keys(n, seed=k)
+    vals = np.arange(n, dtype=np.uint32) * np.uint32(2654435761)
+    ko_ref, vo_ref = oracle_sort_pairs(keys, vals, k)
+    p = rs.plan(n, k, True)
+    assert (p.threads, p.tile_keys) == (1024, 8192)
+    ok, ov = rs.empty_u32(n), rs.empty_u32(n)
+    rs.scatter_kernels_used(reset=True)
+    rs.sort_device(dev(keys), ok, k, vals_in=dev(vals), vals_out=ov)
+    torch.cuda.synchronize()
+    used = rs.scatter_kernels_used(reset=True)
+    assert np.array_equal(host(ok), ko_ref) and np.array_equal(host(ov), vo_ref)
+    assert any(u.startswith("rs_scatter_pairs" if k >= 7 else "rs_scatter_lines") for u in used), used
+
+
 def test_pairs_host_entry():
     n = 70001
     keys = zipf_keys(n, seed=3)
