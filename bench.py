@@ -468,8 +468,9 @@ def main():
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     algo_bytes = bytes_per_key * keys_per_launch
     achieved = algo_bytes / (scatter_ms * 1e-3) / 1e9
-    # the pass's working kernel: the plain variant (the clustered-input twins end in ", 1>" / ", 2>")
-    plain = [k for k in kernels_used if not (k.endswith(", 1>") or k.endswith(", 2>")) or k.startswith("rs_scatter<")]
+    # the pass's working kernel: the plain variant where a clustered-input twin (the same name ending
+    # in ", 1>" instead of ", 0>") was launched beside it
+    plain = [k for k in kernels_used if not (k.endswith(", 1>") and k[:-2] + "0>" in kernels_used)]
     kernel = (plain[-1] if plain else rs.scatter_kernel_name(p)) if not use_dist else \
         "rs_scatter_lines (partition and sort passes)"
     cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel.split('<')[0]}"

@@ -2317,8 +2317,11 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         constexpr int GL = PAIRS ? kGeomLinesPairs : kGeomLines;
         if (geom == GL) {
             if constexpr (PAIRS && (kGeomShape[GL].threads >> BITS) <= 8) {  // (carry slots per thread >= 4)
+                // rank_add_hot's ranking on every pass, uniform keys too: 3.51 vs 3.84 ms per 2^30-pair
+                // pass with rank_add, 3.52 vs 3.78 on Zipf pass 0, 3.63 vs 3.80 on Zipf pass 1
+                // (dev/pairs_lab.hip, round-robin best of 3); one kernel, no clustered twin
                 if (rank == kRankAtomic && aligned16 && !pairs_lines64())
-                    return reg_pairs<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt>();
+                    return reg_pairs<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt, 1>();
             }
             if (rank == kRankAtomic && aligned16)
                 return reg_lines<BITS, kGeomShape[GL].threads, kGeomShape[GL].kpt,
@@ -2516,8 +2519,7 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
             cl = reg_lines<8, 1024, 16, kLineKeys, false, kDigitShift, 3, 1>();
         else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<8, PT, PK, kLineKeysPairs, true, kDigitShift, 2>))
             cl = reg_lines<8, PT, PK, kLineKeysPairs, true, kDigitShift, 2, 1>();
-        else if (fn == reinterpret_cast<void *>(&rs_scatter_pairs<8, PT, PK>))
-            cl = reg_pairs<8, PT, PK, 1>();
+
     }
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
