@@ -22,6 +22,9 @@
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
+#   profiles TAG     the committed profile set: run_profiles.sh for C3, Zipf keys, C4 and C2 (TAG,
+#                    TAG_zipf, TAG_c4, TAG_c2), then kernel traces of the one-rank multi-GPU step, the
+#                    default (direct sort) and the whole protocol (--dist-full)
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R" || exit 1
 mkdir -p gpurun_out
@@ -152,6 +155,22 @@ dist)
         --steps 3 --warmup 1 "$@" > "$R/gpurun_out/prof_dist.log" 2>&1)
     stop_unless_ok $? dist
     tail -c 1500 "$R/gpurun_out/prof_dist.log"
+    ;;
+profiles)
+    tag=$1
+    bash profiles/run_profiles.sh "$tag" || exit $?
+    bash profiles/run_profiles.sh "${tag}_zipf" --dist zipf || exit $?
+    bash profiles/run_profiles.sh "${tag}_c4" --dist zipf --pairs || exit $?
+    bash profiles/run_profiles.sh "${tag}_c2" --keys 67108864 --k 4 || exit $?
+    for v in "" "--dist-full"; do
+        d="$R/gpurun_out/prof_${tag}_dist${v:+_full}"
+        rm -rf "$d"
+        (cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$d" -- \
+            python3 "$R/bench.py" --no-cpu --no-e2e --no-vendor --configs "" --dist-path $v --steps 3 --warmup 1 \
+            > "$d.log" 2>&1)
+        stop_unless_ok $? "dist $v"
+        tail -c 600 "$d.log"
+    done
     ;;
 *)
     echo "unknown experiment: $exp (see the header of dev/lab.sh)"
