@@ -239,8 +239,10 @@ Carve carve(const rsort_plan &p, void *ws) {
 // ------------------------------------------------------------------------------ pass pieces
 // Joint pass (pass p of a joint_plan counting for pass p + 1): one workgroup per chunk counts
 // this pass's table and the joint counts; then the chunks of pass p + 1 (its digit groups, or
-// the cut plan). enable: nullptr, or the previous odd pass's mode: the joint count runs only after
-// whole digit groups (after a cut plan the input is clustered and the count costs more than it saves).
+// the cut plan). enable: nullptr, or the previous odd pass's mode: the joint count runs after whole
+// digit groups and after a cut plan (both leave the joint counts cleared: the copy-mode histogram, the
+// cut plan's scan), not after fixed chunks. After a cut plan the input is clustered: the joint count
+// adds runs of equal pairs once (rs_histogram's run path), so pass 3 gets its own cut plan too.
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                        uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
                        uint32_t *pcounts, hipStream_t s, bool zero_joint) {

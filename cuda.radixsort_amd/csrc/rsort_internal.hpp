@@ -79,7 +79,7 @@ struct HistArgs {
     uint32_t *pcounts;
     uint32_t wide;          // 1: 1024-thread workgroups also with split == 1 (one per chunk, no memset)
     // rs_histogram_joint only: the joint counts [next digit][digit] are added into `joint`
-    // (zeroed); joint_enable == nullptr or *joint_enable == kGroupsWhole turns the joint count on.
+    // (zeroed); joint_enable == nullptr or *joint_enable != kGroupsFixed turns the joint count on.
     uint32_t *joint;
     const uint32_t *joint_enable;
 };

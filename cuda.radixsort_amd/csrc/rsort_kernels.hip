@@ -363,27 +363,25 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         }
     };
     auto add = [&](uint32_t x) { add_pair((x >> s0) & (R - 1u), (x >> s1) & (R - 1u), 1u); };
-    // clustered input (runs of equal keys: sorted or duplicate-heavy data) sends a wave's lanes to
-    // one counter, where they serialise (all-equal keys: 64 lanes, ~128 cycles per instruction).
-    // Per 16-B quad: when most lanes hold 4 equal pairs, each such lane's 4 become one add of 4,
-    // and one lane adds for all lanes sharing the first lane's pair (as count_add); uniform keys
-    // pay one compare chain and one ballot per quad (the plain histogram's same4 test)
-    const uint32_t pmask = 0xFFFFu << s0;  // the pair's 16 bits (s0 <= 16 for a joint pass)
-    auto same4_of = [&](const u32x4 &q) { return (((q.x ^ q.y) | (q.x ^ q.z) | (q.x ^ q.w)) & pmask) == 0u; };
-    auto add4 = [&](const u32x4 &q) {
-        const uint32_t p0 = (q.x >> s0) & 0xFFu | ((q.x >> s1) & 0xFFu) << 8;
-        const bool same4 = same4_of(q);
-        if (!same4) {
-            add(q.x);
-            add(q.y);
-            add(q.z);
-            add(q.w);
+    // Clustered input (runs of equal keys: sorted or duplicate-heavy data, and every pass after a cut
+    // plan, whose input holds the copies of a key contiguously) sends many lanes of one instruction to
+    // one counter, where returning adds serialise (all-equal keys: 64 lanes, ~128 cycles per
+    // instruction). There each component of a batch of quads (lane l holds keys 4l .. 4l + 3, so lanes
+    // l and l + 1 hold keys 4 apart) is added by runs: lanes holding the same pair as the lane below
+    // continue its run, and only a run's first lane adds (the run's length, one returning add).
+    // Uniform keys take the plain adds after one test per batch (the first quad's first and last keys).
+    auto pair_of = [&](uint32_t x) { return (x >> s0) & 0xFFu | ((x >> s1) & 0xFFu) << 8; };
+    auto add_run = [&](uint32_t x) {
+        const uint32_t pr = pair_of(x);
+        // the lane below's pair (wave_shr:1; lane 0 gets ~pr: it starts a run)
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)~pr, (int)pr, 0x138, 0xF, 0xF, false);
+        const bool cont = prev == pr;
+        const uint64_t brk = __ballot(!cont) | ~__ballot(true);  // (inactive lanes end every run)
+        if (!cont) {
+            const uint64_t above = brk & ~((2ull << lane_id()) - 1ull);
+            const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : 64u;
+            add_pair(pr & 0xFFu, pr >> 8, end - lane_id());
         }
-        // lanes with 4 equal pairs: the first such lane's pair once for all lanes sharing it
-        const uint32_t pa = __builtin_amdgcn_readfirstlane(same4 ? p0 : 0xFFFFFFFFu);
-        const uint64_t ma = __ballot(same4 && p0 == pa);
-        if (same4 && p0 != pa) add_pair(p0 & 0xFFu, p0 >> 8, 4u);
-        if (same4 && lane_id() == (uint32_t)__builtin_ctzll(ma)) add_pair(p0 & 0xFFu, p0 >> 8, 4u * (uint32_t)__popcll(ma));
     };
     const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
@@ -402,8 +400,8 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
                 const uint32_t v = v0 + u * THREADS;
                 q[u] = v < nvec ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
             }
-            // one clustering test per batch (the first quad): uniform keys take the plain adds
-            if (__popcll(__ballot(same4_of(q[0]))) < 32) {
+            // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
+            if (__popcll(__ballot(pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (v0 + u * THREADS < nvec) {
@@ -416,7 +414,12 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (v0 + u * THREADS < nvec) add4(q[u]);
+                    if (v0 + u * THREADS < nvec) {
+                        add_run(q[u].x);
+                        add_run(q[u].y);
+                        add_run(q[u].z);
+                        add_run(q[u].w);
+                    }
                 }
             }
         }
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
         return;
     }
     if constexpr (JOINT) {
-        if (a.joint_enable == nullptr || *a.joint_enable == kGroupsWhole) {
+        if (a.joint_enable == nullptr || *a.joint_enable != kGroupsFixed) {
             hist_joint_body<THREADS>(a, s_h, c, sub, S);
             return;
         }
@@ -822,7 +825,7 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     __shared__ uint32_t s_cf[R], s_cl[R];          // cut group: first and last chunk
     __shared__ uint32_t s_slot[R];                 // counted pieces' slots
     const uint32_t t = threadIdx.x;
-    if (enable != nullptr && *enable != kGroupsWhole) {  // no joint count this pass
+    if (enable != nullptr && *enable == kGroupsFixed) {  // no joint count this pass
         if (t == 0) bounds[0] = kGroupsFixed;
         return;
     }
