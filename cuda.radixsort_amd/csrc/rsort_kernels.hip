@@ -1719,7 +1719,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 // rs_scatter_lines.
 // (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
 // the next tile's loads issued before the rank loop instead of after it, OPT & 4 keys and values
-// staged interleaved)
+// staged interleaved, OPT & 8 step 4 deferred to after the next tile's rank phase)
 template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
@@ -1740,6 +1740,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     // [0, CAP) segments; [CAP, CAP + 32) the last tail read's overrun; CAP + 32 the padding sink
     // OPT & 4: one interleaved {key, value} array (8-B stores per pair) instead of two
     constexpr bool IL = (OPT & 4) != 0;
+    constexpr bool DEFER = (OPT & 8) != 0;
     __shared__ __attribute__((aligned(16))) uint32_t s_k[IL ? 4 : CAP + 36];
     __shared__ __attribute__((aligned(16))) uint32_t s_v[IL ? 4 : CAP + 36];
     __shared__ __attribute__((aligned(16))) uint2 s_kv[IL ? CAP + 36 : 2];
@@ -1844,11 +1845,48 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
         }
     };
 
+    RS_STAMP_DECL
+    // ---- 4. (of a tile) the tails back into the carry registers (the quads holding any); whole lines
+    //      out. DEFER: run after the NEXT tile's rank phase instead of at the end of the tile.
+    auto output = [&](const uint32_t S, const uint32_t wl, const uint32_t pending, const uint32_t nlines,
+                      const uint32_t cnt) {
+        {
+            const uint32_t tl0 = S + wl * G + sub * CPT;  // quad-aligned
+            const uint32_t ncarry = pending - wl * G;
+#pragma unroll
+            for (uint32_t i = 0; i < CPT; i += 4) {
+                if (sub * CPT + i >= ncarry) break;
+                u32x4 kq, vq;
+                if constexpr (IL) {
+                    const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i]);
+                    const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i + 2]);
+                    kq = u32x4{p01.x, p01.z, p23.x, p23.z};
+                    vq = u32x4{p01.y, p01.w, p23.y, p23.w};
+                } else {
+                    kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+                    vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
+                }
+                ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
+                cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
+            }
+        }
+        const uint32_t nq = nlines * QPL;
+        for (uint32_t item = t; item < nq; item += 2 * THREADS) {
+            store_item(item);
+            if (item + THREADS < nq) store_item(item + THREADS);
+        }
+        RS_STAMP(4);
+        if (wl > 0) inv = 0;
+        carry = pending - wl * G;
+        g_run += cnt;
+    };
+    uint32_t pS = 0, pwl = 0, ppend = 0, pnl = 0, pcnt = 0;  // DEFER: the staged tile's step-4 state
+    bool have_prev = false;
+
     // The tile step. PF = 1: the next tile's loads go into nkey at the end of the rank phase and
     // move into key at the end of the step. PF = 2: two register sets alternate (the loop is unrolled
     // by two); a tile's set takes the loads of the tile two ahead as soon as it is staged.
     uint32_t hotd = 0xFFFFFFFFu;
-    RS_STAMP_DECL
     auto tile_step = [&](const uint64_t tb, uint32_t (&key)[KPT], uint32_t (&val)[KPT]) {
             const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
             const bool full = valid == T && head == 0;
@@ -1882,10 +1920,18 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
+            RS_STAMP(5);
             if constexpr (PF == 1 && !(OPT & 2)) {
                 if (nb < cend) load_tile(nb, nkey, nval);
             }
-            // (the previous tile's step 4 has read the bitmap: behind the barrier below)
+            if constexpr (DEFER) {
+                // the previous tile's output: its stores then have steps 2-3 of this tile to drain
+                // before the next vmcnt wait (at the next rank phase), instead of none
+                if (have_prev) output(pS, pwl, ppend, pnl, pcnt);
+                have_prev = true;
+            }
+            // (the previous tile's step 4 has read the bitmap, records and staging area: behind the
+            // barrier below)
             __syncthreads();
             RS_STAMP(0);
 
@@ -1989,36 +2035,15 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             __syncthreads();
             RS_STAMP(3);
 
-            // ---- 4. the tails back into the carry registers (the quads holding any); whole lines out
-            {
-                const uint32_t tl0 = S + wl * G + sub * CPT;  // quad-aligned
-                const uint32_t ncarry = pending - wl * G;
-    #pragma unroll
-                for (uint32_t i = 0; i < CPT; i += 4) {
-                    if (sub * CPT + i >= ncarry) break;
-                    u32x4 kq, vq;
-                    if constexpr (IL) {
-                        const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i]);
-                        const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i + 2]);
-                        kq = u32x4{p01.x, p01.z, p23.x, p23.z};
-                        vq = u32x4{p01.y, p01.w, p23.y, p23.w};
-                    } else {
-                        kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
-                        vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
-                    }
-                    ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
-                    cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
-                }
+            if constexpr (DEFER) {
+                pS = S;
+                pwl = wl;
+                ppend = pending;
+                pnl = nlines;
+                pcnt = cnt;
+            } else {
+                output(S, wl, pending, nlines, cnt);
             }
-            const uint32_t nq = nlines * QPL;
-            for (uint32_t item = t; item < nq; item += 2 * THREADS) {
-                store_item(item);
-                if (item + THREADS < nq) store_item(item + THREADS);
-            }
-            RS_STAMP(4);
-            if (wl > 0) inv = 0;
-            carry = pending - wl * G;
-            g_run += cnt;
             if constexpr (PF == 1) {
     #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
@@ -2038,6 +2063,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             tile_step(tb, keyA, valA);
             if (tb + T < cend) tile_step(tb + T, keyB, valB);
         }
+    }
+    if constexpr (DEFER) {
+        if (have_prev) output(pS, pwl, ppend, pnl, pcnt);
     }
     // ---- chunk end: the carries (slots inv .. carry - 1 from the line at g_run - carry)
     if (cbeg < cend) {

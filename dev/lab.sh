@@ -19,6 +19,8 @@
 #                    dev/ktall.py / dev/ktsum.py read it)
 #   variants V...    dev/var_V.so (dev/build_variant.sh) over the box's librsort.so in turn: kernel
 #                    traces of the C3, Zipf-keys and all-equal benches
+#   ab V [CONFIGS]   bench.py's configs block (default zipf,c4) on the built librsort.so, then on
+#                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels for an A/B)
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
@@ -132,6 +134,22 @@ variants)
         kt "c3_$v"
         kt "z_$v" --dist zipf
         kt "e_$v" --dist equal
+    done
+    ;;
+ab)
+    # bench.py's configs block (zipf, c4, or $2) on the box's librsort.so, then on dev/var_$1.so
+    v=$1
+    for side in new "$v"; do
+        [ "$side" = new ] || cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so
+        run_bench "ab_$side" --steps 2 --warmup 1 --keys 16777216 --no-cpu --no-vendor --no-e2e \
+            --configs "${2:-zipf,c4}" > /dev/null
+        python3 - "$side" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/ab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+for k, c in d["configs"].items():
+    print("%-6s %-5s %8.3f ms/sort  hist %.3f  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], k, c["ms_per_sort"],
+          c["phases_ms_per_sort"]["histogram"], c["scatter"]["avg_launch_ms"], c["scatter"]["frac"], c["verified"]))
+PY
     done
     ;;
 prof)
