@@ -196,6 +196,32 @@ def test_joint_count_clustered(kind):
     assert np.array_equal(y, oracle_sort(x, 8))
 
 
+@pytest.mark.parametrize("kind", ["equal", "hot_runs", "zipf"])
+def test_joint_count_after_cut_pass(kind):
+    """Pass 2's joint count after a cut pass 1 (rs_histogram JOINT on clustered input) at 2^25 - 12345
+    keys, 256 chunks of ~131K keys: a pair's count in one chunk runs to 2^17 (all-equal keys: the
+    16-bit counters spill four times), runs of one pair mix with plain batches (hot runs), and the C4
+    key distribution."""
+    n = 2048 * LINE_TILE - 12345
+    rng = np.random.default_rng(41)
+    if kind == "equal":
+        x = np.full(n, 0x0BADF00D, dtype=np.uint32)
+        x[rng.integers(0, n, 1000)] = rng.integers(0, 1 << 32, 1000, dtype=np.uint64).astype(np.uint32)
+    elif kind == "hot_runs":
+        x = uniform_keys(n, seed=41)
+        x[rng.random(n) < 0.3] = np.uint32(0xC0FFEE11)  # one group of ~30 % of the keys: a cut plan
+        lens = rng.integers(1, 2000, n // 1000 + 2)
+        vals = rng.integers(0, 1 << 16, lens.size, dtype=np.uint64).astype(np.uint32) << np.uint32(16)
+        hi = np.repeat(vals, lens)[:n]
+        m = rng.random(n) < 0.5
+        x[m] = (x[m] & np.uint32(0xFFFF)) | hi[m]  # long runs of one (digit 2, digit 3) pair
+    else:
+        x = zipf_keys(n, seed=41)
+    y, flags = run(x, group_plan(n))
+    assert flags[0] == 2
+    assert np.array_equal(y, oracle_sort(x, 8))
+
+
 @pytest.mark.parametrize("pairs", [False, True])
 def test_clustered_kernels(pairs):
     """Unbalanced groups select the clustered-input kernels (rank_add_hot) for passes 1..3. Input
