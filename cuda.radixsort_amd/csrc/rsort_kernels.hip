@@ -105,6 +105,16 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
+// Lane count of a wave-uniform mask as an opaque 32-bit scalar. `__popcll(m) < c` is folded into a
+// 64-bit unsigned compare of the i64 popcount, which the SALU cannot do (no s_cmp_lt_u64): it went
+// to the VALU (v_cmp_lt_u64 on SGPR operands) on every key of the rank loops. s_bcnt1 into a 32-bit
+// SGPR keeps the test on the SALU (s_cmp + s_cbranch_scc).
+__device__ __forceinline__ uint32_t wave_count(uint64_t m) {
+    uint32_t c;
+    asm("s_bcnt1_i32_b64 %0, %1" : "=s"(c) : "s"(m));
+    return c;
+}
+
 // Lane-ordered returning LDS add of 1 to cnt[d] for every lane of a wave (the kRankAtomic
 // premise: same-address lanes are served in lane order, so lane l gets old + #lower lanes with
 // digit d). Same-address lanes serialise in the LDS (about 2 cycles each: 127 cycles when all 64
@@ -117,7 +127,7 @@ __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) -
 __device__ __forceinline__ uint32_t rank_add(uint32_t *cnt, uint32_t d) {
     const uint32_t da = __builtin_amdgcn_readfirstlane(d);
     const uint64_t ma = __ballot(d == da);
-    if (__popcll(ma) < 16) return atomicAdd(&cnt[d], 1u);
+    if (wave_count(ma) < 16) return atomicAdd(&cnt[d], 1u);
     const uint32_t la = (uint32_t)__builtin_ctzll(ma);
     uint32_t o = 0;
     if (d != da) o = atomicAdd(&cnt[d], 1u);
@@ -130,7 +140,7 @@ __device__ __forceinline__ uint32_t rank_add(uint32_t *cnt, uint32_t d) {
 __device__ __forceinline__ void count_add(uint32_t *cnt, uint32_t d, uint32_t inc = 1u) {
     const uint32_t da = __builtin_amdgcn_readfirstlane(d);
     const uint64_t ma = __ballot(d == da);
-    if (__popcll(ma) < 16) {
+    if (wave_count(ma) < 16) {
         atomicAdd(&cnt[d], inc);
         return;
     }
@@ -159,12 +169,12 @@ __device__ __forceinline__ uint32_t agg_add(uint32_t *cnt, uint32_t d, uint32_t 
 __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint32_t &hot) {
     const uint32_t da = __builtin_amdgcn_readfirstlane(d);
     const uint64_t ma = __ballot(d == da);
-    if (__popcll(ma) >= 16) {
+    if (wave_count(ma) >= 16) {
         hot = da;
         return agg_add(cnt, d, da, ma);
     }
     const uint64_t mh = __ballot(d == hot);
-    if (__popcll(mh) >= 8) return agg_add(cnt, d, hot, mh);
+    if (wave_count(mh) >= 8) return agg_add(cnt, d, hot, mh);
     return atomicAdd(&cnt[d], 1u);
 }
 
@@ -401,7 +411,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
                 q[u] = v < nvec ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
             }
             // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
-            if (__popcll(__ballot(pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
+            if (wave_count(__ballot(pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (v0 + u * THREADS < nvec) {
@@ -504,7 +514,7 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
                     if (v0 + u * THREADS < nvec) {
                         const uint32_t dx = dig(q[u].x), dy = dig(q[u].y), dz = dig(q[u].z), dw = dig(q[u].w);
                         const bool same4 = dx == dy && dy == dz && dz == dw;
-                        if (__popcll(__ballot(same4)) >= 32) {
+                        if (wave_count(__ballot(same4)) >= 32) {
                             // clustered input (runs of equal keys, e.g. duplicates after a pass): one
                             // add of 4 per lane, lanes sharing the common digits together
                             if (same4) {
@@ -1957,6 +1967,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             if (t < NBW) s_bits[t] = 0u;
             uint32_t tot;
             const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
+            RS_STAMP(7);
             const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
             const uint32_t nlines = tot >> 16;
             if (sub < (uint32_t)W) {
@@ -1990,6 +2001,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
                 }
             }
+            RS_STAMP(6);
             __syncthreads();
             RS_STAMP(1);
 

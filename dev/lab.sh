@@ -19,8 +19,8 @@
 #                    dev/ktall.py / dev/ktsum.py read it)
 #   variants V...    dev/var_V.so (dev/build_variant.sh) over the box's librsort.so in turn: kernel
 #                    traces of the C3, Zipf-keys and all-equal benches
-#   ab V [CONFIGS]   bench.py's configs block (default zipf,c4) on the built librsort.so, then on
-#                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels for an A/B)
+#   ab V [CONFIGS]   the C3 line and the configs block (default zipf,c4): the built librsort.so and
+#                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels), alternating twice
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
@@ -137,20 +137,27 @@ variants)
     done
     ;;
 ab)
-    # bench.py's configs block (zipf, c4, or $2) on the box's librsort.so, then on dev/var_$1.so
+    # the C3 line and bench.py's configs block (zipf, c4, or $2): the box's librsort.so ("new") and
+    # dev/var_$1.so, alternating twice
     v=$1
-    for side in new "$v"; do
-        [ "$side" = new ] || cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so
-        run_bench "ab_$side" --steps 2 --warmup 1 --keys 16777216 --no-cpu --no-vendor --no-e2e \
+    cp cuda.radixsort_amd/librsort.so gpurun_out/ab_new.so
+    for side in new "$v" new "$v"; do
+        if [ "$side" = new ]; then cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so; else cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so; fi
+        run_bench "ab_$side" --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
             --configs "${2:-zipf,c4}" > /dev/null
         python3 - "$side" <<'PY'
 import json, sys
 d = json.loads(open(f"gpurun_out/ab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+r = d["roofline"]
+print("%-6s C3    %8.3f ms/sort  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], d["ms_per_step"],
+      r["avg_launch_ms"], r["frac"], d["verified"]))
 for k, c in d["configs"].items():
     print("%-6s %-5s %8.3f ms/sort  hist %.3f  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], k, c["ms_per_sort"],
           c["phases_ms_per_sort"]["histogram"], c["scatter"]["avg_launch_ms"], c["scatter"]["frac"], c["verified"]))
 PY
     done
+    cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/ab_new.so
     ;;
 prof)
     tag=$1

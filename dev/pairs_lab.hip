@@ -148,18 +148,10 @@ int main(int argc, char **argv) {
     std::vector<Var> vars = {
         {"rs_scatter_lines 64-B 512 x 16", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2><<<g, 512>>>(x); }, 1e9f, {}},
-        {"rs_scatter_lines 64-B 1024 x 8", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_lines<8, 1024, 8, kLineKeysPairs, true, kDigitShift, 2><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_pairs<8, 1024, 8><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8, CL", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_pairs<8, 1024, 8, 1><<<g, 1024>>>(x); }, 1e9f, {}},
-        {"rs_scatter_pairs 128-B 1024 x 8, CL deferred out", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_pairs<8, 1024, 8, 1, 1, 8><<<g, 1024>>>(x); }, 1e9f, {}},
-        {"rs_scatter_pairs 128-B 1024 x 8, deferred out", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_pairs<8, 1024, 8, 0, 1, 8><<<g, 1024>>>(x); }, 1e9f, {}},
-        {"rs_scatter_pairs 128-B 1024 x 8, CL deferred il", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_pairs<8, 1024, 8, 1, 1, 12><<<g, 1024>>>(x); }, 1e9f, {}},
     };
     const int rounds = env_int("PL_ROUNDS", 3);
     std::vector<uint32_t> refk(n), refv(n), gk(n), gv(n);
@@ -197,8 +189,8 @@ int main(int argc, char **argv) {
         double tot = 0;
         for (uint32_t c = 0; c < chunks; ++c) tot += (double)v.st[c * 8];
         if (tot > 0) {  // rs_scatter_pairs: per-phase cycles per tile (thread 0, mean over chunks)
-            printf("  cycles/tile (sync, seg, rec, stage, out, rank):");
-            for (int i = 0; i < 6; ++i) {
+            printf("  cycles/tile (sync, seg-barrier, rec, stage, out, rank, seg-after-scan, seg-to-scan):");
+            for (int i = 0; i < 8; ++i) {
                 double s2 = 0;
                 for (uint32_t c = 0; c < chunks; ++c) s2 += (double)v.st[c * 8 + i];
                 printf(" %.0f", s2 / chunks / tpc);
