@@ -178,6 +178,48 @@ __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint
     return atomicAdd(&cnt[d], 1u);
 }
 
+// slots per issue batch of the deferred ranking (0: rank_add / rank_add_hot slot by slot), per kernel
+#ifndef RSORT_DEFER_KEYS_CL
+#define RSORT_DEFER_KEYS_CL 2
+#endif
+#ifndef RSORT_DEFER_KEYS_PLAIN
+#define RSORT_DEFER_KEYS_PLAIN 0
+#endif
+#ifndef RSORT_DEFER_PAIRS
+#define RSORT_DEFER_PAIRS 4
+#endif
+// rank_add_hot in two halves, so a tile's KPT slots issue their returning adds back to back and
+// wait for the LDS once: hot_issue picks the slot's aggregated digit c (~0u: none) and its lanes m
+// exactly as rank_add_hot and issues the slot's one add; hot_rank, after every slot is issued, turns
+// the returns into ranks (the aggregated lanes read their leader's return).
+template <bool HOT>
+__device__ __forceinline__ uint32_t hot_issue(uint32_t *cnt, uint32_t d, uint32_t &hot, uint32_t &c, uint64_t &m) {
+    const uint32_t da = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t ma = __ballot(d == da);
+    if (wave_count(ma) >= 16) {
+        hot = da;
+        c = da;
+        m = ma;
+    } else if (!HOT) {
+        c = 0xFFFFFFFFu;
+        m = 0ull;
+    } else {
+        const uint64_t mh = __ballot(d == hot);
+        const bool agg = wave_count(mh) >= 8;
+        c = agg ? hot : 0xFFFFFFFFu;
+        m = agg ? mh : 0ull;
+    }
+    const bool mine = d == c;
+    uint32_t o = 0;
+    if (!mine || lane_id() == (uint32_t)__builtin_ctzll(m)) o = atomicAdd(&cnt[d], mine ? (uint32_t)__popcll(m) : 1u);
+    return o;
+}
+__device__ __forceinline__ uint32_t hot_rank(uint32_t o, uint32_t d, uint32_t c, uint64_t m) {
+    if (c == 0xFFFFFFFFu) return o;
+    const uint32_t base = __builtin_amdgcn_readlane(o, (uint32_t)__builtin_ctzll(m));
+    return d == c ? base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) : o;
+}
+
 // Row stride of per-wave digit counters [wave][digit] read column-wise by digit groups: TPD threads
 // per digit, thread `sub` taking rows sub * WPT .. + WPT - 1. With rows R apart (R a multiple of
 // 64) the TPD threads of a digit hit one bank; a stride with WPT * RS = 64 / TPD (mod 64) puts the
@@ -405,16 +447,18 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         constexpr int U = 4;
         for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
             u32x4 q[U];
+            bool ok[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t v = v0 + u * THREADS;
-                q[u] = v < nvec ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
+                ok[u] = v < nvec;
+                q[u] = ok[u] ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
             }
             // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
-            if (wave_count(__ballot(pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
+            if (wave_count(__ballot(ok[0] && pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (v0 + u * THREADS < nvec) {
+                    if (ok[u]) {
                         add(q[u].x);
                         add(q[u].y);
                         add(q[u].z);
@@ -424,7 +468,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             } else {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (v0 + u * THREADS < nvec) {
+                    if (ok[u]) {
                         add_run(q[u].x);
                         add_run(q[u].y);
                         add_run(q[u].z);
@@ -1478,7 +1522,25 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
         for (int i = 0; i < (PD ? (KPT + 7) / 8 : 1); ++i) dpk[i] = 0;
         uint32_t nkey[KPT];
         uint32_t nval[PAIRS ? KPT : 1];
-        if (full) {
+        constexpr int DB = CL ? RSORT_DEFER_KEYS_CL : RSORT_DEFER_KEYS_PLAIN;
+        if (full && DB > 0 && !PD) {
+            // deferred ranking: batches of DB slots issue their adds, then turn the returns into ranks
+            static_assert(DB == 0 || KPT % (DB > 0 ? DB : 1) == 0, "whole batches");
+#pragma unroll
+            for (int j0 = 0; j0 < KPT; j0 += (DB > 0 ? DB : 1)) {
+                uint32_t o[DB > 0 ? DB : 1], cc[DB > 0 ? DB : 1];
+                uint64_t mm[DB > 0 ? DB : 1];
+#pragma unroll
+                for (int u = 0; u < DB; ++u)
+                    o[u] = hot_issue<CL != 0>(&s_cnt[w * RS], dig(key[j0 + u]), hotd, cc[u], mm[u]);
+#pragma unroll
+                for (int u = 0; u < DB; ++u) {
+                    const int j = j0 + u;
+                    const uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
+                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                }
+            }
+        } else if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 // (measured: rank_add's aggregation is ~2% faster than plain lane-ordered adds even
@@ -1914,7 +1976,26 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             if constexpr (PF == 1 && (OPT & 2)) {
                 if (nb < cend) load_tile(nb, nkey, nval);
             }
-            if (full) {
+            constexpr int DB = RSORT_DEFER_PAIRS;
+            if (full && DB > 0) {
+                // deferred ranking (hot_issue / hot_rank): the slots' adds back to back, one LDS wait
+                // per batch of DB slots (C4: 3.45 vs 3.48 ms per pass, dev/lab.sh ab)
+                static_assert(DB == 0 || KPT % (DB > 0 ? DB : 1) == 0, "whole batches");
+    #pragma unroll
+                for (int j0 = 0; j0 < KPT; j0 += (DB > 0 ? DB : 1)) {
+                    uint32_t o[DB > 0 ? DB : 1], cc[DB > 0 ? DB : 1];
+                    uint64_t mm[DB > 0 ? DB : 1];
+    #pragma unroll
+                    for (int u = 0; u < DB; ++u)
+                        o[u] = hot_issue<CL != 0>(&s_cnt[w * RS], dig(key[j0 + u]), hotd, cc[u], mm[u]);
+    #pragma unroll
+                    for (int u = 0; u < DB; ++u) {
+                        const int j = j0 + u;
+                        const uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
+                        rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+                    }
+                }
+            } else if (full) {
     #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t dj = dig(key[j]);
@@ -2421,10 +2502,10 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
 // that hit the same address in ascending lane order. The probe replays the production conditions of
 // the line kernels: the 1024-thread shape of the k = 8 keys and pairs kernels (counter rows
 // counter_stride = 260 words apart) and the 512-thread shape of the partition kernels (rows 264
-// apart at 256 digits), the SAME device functions the kernels
-// instantiate -- rank_add (any exec mask) and rank_add_hot with its agg_add paths (full waves, as in
-// the kernels' full tiles) -- on digit ranges 1..256, runs of equal digits (with several runs sharing
-// a digit), a run crossing the slot, partial exec masks; and checks every
+// apart at 256 digits), the SAME device functions the kernels instantiate -- rank_add (any exec
+// mask), rank_add_hot with its agg_add paths and the deferred hot_issue / hot_rank (full waves, as
+// in the kernels' full tiles) -- on digit ranges 1..256, runs of equal digits (with several runs
+// sharing a digit), a run crossing the slot, partial exec masks; and checks every
 // returned rank against old value + #lower active lanes with the same digit (a register-only count).
 // Any mismatch makes the library use ballots.
 template <int THREADS>
@@ -2457,8 +2538,9 @@ __global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
             case 6: d = (hw + (lane / L) % 3) % 256; break;           // runs, several sharing a digit
             default: d = (hw + (lane / (1u + hw % 5u)) * 7u) % 256;   // many short runs (> 32: the fallback)
         }
-        // which ranking: rank_add (partial exec masks too), rank_add_hot (full waves, as in the kernels)
-        const uint32_t fn = (it / 8) % 2;
+        // which ranking: rank_add (partial exec masks too), rank_add_hot, and the deferred hot_issue +
+        // hot_rank with and without the hot candidate (full waves, as in the kernels)
+        const uint32_t fn = (it / 8) % 4;
         const bool active = fn != 0 || (it % 3 == 0) || ((h >> 7) % 4 != 0);
         const uint32_t before = s_cnt[w * RS + d];
         uint32_t below = 0;
@@ -2469,7 +2551,18 @@ __global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
         }
         __builtin_amdgcn_wave_barrier();
         if (active) {
-            const uint32_t got = fn == 0 ? rank_add(&s_cnt[w * RS], d) : rank_add_hot(&s_cnt[w * RS], d, hot);
+            uint32_t got;
+            if (fn == 0) {
+                got = rank_add(&s_cnt[w * RS], d);
+            } else if (fn == 1) {
+                got = rank_add_hot(&s_cnt[w * RS], d, hot);
+            } else {
+                uint32_t c;
+                uint64_t m;
+                const uint32_t o = fn == 2 ? hot_issue<true>(&s_cnt[w * RS], d, hot, c, m)
+                                           : hot_issue<false>(&s_cnt[w * RS], d, hot, c, m);
+                got = hot_rank(o, d, c, m);
+            }
             nbad += got != before + below;
         }
         __builtin_amdgcn_wave_barrier();
