@@ -1791,7 +1791,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
 // rs_scatter_lines.
 // (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
 // the next tile's loads issued before the rank loop instead of after it, OPT & 4 keys and values
-// staged interleaved, OPT & 8 step 4 deferred to after the next tile's rank phase)
+// staged interleaved, OPT & 8 step 4 deferred to after the next tile's rank phase,
+// OPT & 16 / 32 the next tile's loads issued after step 2 / step 3 instead of after the rank phase)
 template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
 __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
@@ -2012,7 +2013,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                 }
             }
             RS_STAMP(5);
-            if constexpr (PF == 1 && !(OPT & 2)) {
+            if constexpr (PF == 1 && !(OPT & (2 | 16 | 32))) {
                 if (nb < cend) load_tile(nb, nkey, nval);
             }
             if constexpr (DEFER) {
@@ -2085,6 +2086,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             RS_STAMP(6);
             __syncthreads();
             RS_STAMP(1);
+            if constexpr (PF == 1 && (OPT & 16)) {
+                if (nb < cend) load_tile(nb, nkey, nval);
+            }
 
             // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
             //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
@@ -2127,6 +2131,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             }
             __syncthreads();
             RS_STAMP(3);
+            if constexpr (PF == 1 && (OPT & 32)) {
+                if (nb < cend) load_tile(nb, nkey, nval);
+            }
 
             if constexpr (DEFER) {
                 pS = S;
