@@ -317,20 +317,100 @@ def run_config(name, c, dev, reps, n_override=0):
     return res
 
 
+def self_launch(a) -> int:
+    """`--gpus N` (N > 1) started plainly, without torch.distributed.run: start the N ranks as ONE
+    child `python -m torch.distributed.run` (127.0.0.1, a free port) running this same command line,
+    and return its exit code. This process never initialises HIP (device_count() does not) and never
+    re-execs; the children inherit stdout, so rank 0's JSON line is this command's output."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (RCCL over dmabuf IPC on these hosts)
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _template_args(name):
+    return [x.strip() for x in name.split("<", 1)[1].rstrip(">").split(",")] if "<" in name else []
+
+
+def is_partition_kernel(name):
+    """A multi-GPU partition's scatter instance (splitter digits: DMODE = kDigitSplit = 1, template
+    argument 5 of rs_scatter / rs_scatter_lines; rs_scatter_pairs never partitions)."""
+    args = _template_args(name)
+    return name.split("<")[0] in ("rs_scatter", "rs_scatter_lines") and len(args) > 5 and args[5] == "1"
+
+
+def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt):
+    """The N-GPU block of the line: per-phase ms (mean over the profiled steps per rank, max over
+    ranks), the exchange's bytes per rank and per peer link, and the local sort's and the partition's
+    own scatter rooflines. per_rank: every rank's list of rsort_multi_stats dicts (one per step)."""
+    ph = ("ms_plan", "ms_partition", "ms_exchange", "ms_local_sort", "ms_total")
+    means = [{k: float(np.mean([st[k] for st in steps])) for k in ph} for steps in per_rank]
+    last = [steps[-1] for steps in per_rank]
+    bpk = last[0]["bytes_per_key"]
+    sent = [sum(x["send_keys"][p] for p in range(world) if p != r) * bpk for r, x in enumerate(last)]
+    recv = [sum(x["recv_keys"][p] for p in range(world) if p != r) * bpk for r, x in enumerate(last)]
+    own = [x["send_keys"][r] * bpk for r, x in enumerate(last)]
+    links = []  # (src, dst, bytes, GB/s over the source rank's exchange phase)
+    for r, x in enumerate(last):
+        for p in range(world):
+            if p != r and x["send_keys"][p]:
+                b = x["send_keys"][p] * bpk
+                links.append((r, p, b, b / (means[r]["ms_exchange"] * 1e-3) / 1e9 if means[r]["ms_exchange"] else None))
+    rates = [l[3] for l in links if l[3]]
+    ex_ms = max(m["ms_exchange"] for m in means)
+
+    def roof(t, what):
+        if not t["launches"]:
+            return None
+        ms = t["ms"] / t["launches"]
+        algo = 8 * t["keys"] / t["launches"] * (2 if last[0]["bytes_per_key"] == 8 else 1)
+        return {"what": what, "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": int(algo),
+                "achieved": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "launches_per_step": t["launches"]}
+
+    return {
+        "transport": transport,
+        "rccl_world": rank_of_stats.get("rccl_world"),
+        "transport_world": int(last[0]["world"]),
+        "halves": int(last[0]["halves"]), "exchange_rounds": int(last[0]["rounds"]),
+        "phases_ms_per_step": {k[3:]: round(max(m[k] for m in means), 4) for k in ph},
+        "phases_ms_per_rank": [{k[3:]: round(m[k], 4) for k in ph} for m in means],
+        "keys_out_per_rank": [int(x["n_out"]) for x in last],
+        "exchange": {"bytes_per_key": int(bpk), "bytes_sent_per_rank": sent, "bytes_recv_per_rank": recv,
+                     "own_range_bytes_per_rank": own,
+                     "GBs_out_per_rank": [round(b / (m["ms_exchange"] * 1e-3) / 1e9, 2) if m["ms_exchange"] else None
+                                          for b, m in zip(sent, means)],
+                     "link_GBs": {"min": round(min(rates), 2), "mean": round(float(np.mean(rates)), 2),
+                                  "max": round(max(rates), 2), "links": len(rates)} if rates else None,
+                     "busiest_link_bytes": max((l[2] for l in links), default=0),
+                     "ms": round(ex_ms, 4)},
+        "local_sort_scatter": roof(sc, "the local sort's scatter passes (rank 0, 8 B/key keys, 16 B/key pairs)"),
+        "partition_scatter": roof(pt, "the key-range partition's scatter (rank 0, splitter digits)"),
+    }
+
+
 def main():
     a = parse()
+    # --gpus N without a launcher: start the N ranks here (before anything touches the GPU)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    # RSORT_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on fewer GPUs
-    # (multi.py with a host-side exchange; timings meaningless). The driver's runs use RCCL.
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; running {world} ranks", file=sys.stderr)
+    # RSORT_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on fewer GPUs (the C
+    # protocol over a gloo host transport; timings meaningless). The driver's runs use RCCL.
     rehearsal = os.environ.get("RSORT_BENCH_BACKEND", "") == "gloo"
     if rehearsal:
         local = local % max(1, torch.cuda.device_count())
-        a.dist_impl = "torch"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or a.dist_path
@@ -367,12 +447,22 @@ def main():
     p = rs.plan(n, a.k, a.pairs, a.tiles_per_chunk)
 
     comm = None
+    host_tr = None
+    transport = None
+    rccl_world = None
     if use_dist and a.dist_impl == "c":
         rs.set_multi_options((rs.MULTI_FULL if a.dist_full else 0) | (rs.MULTI_OVERLAP if a.dist_overlap else 0))
-        uid = [rs.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        with stdout_to_stderr():
-            comm = rs.RcclComm(world, rank, uid[0])
+        if rehearsal:
+            import multi
+            host_tr = multi.host_transport()
+            comm = host_tr.transport
+            transport = f"gloo host transport (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s))"
+        else:
+            uid = [rs.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            with stdout_to_stderr():
+                comm = rs.RcclComm(world, rank, uid[0])
+            transport = "RCCL (rsort_u32_multi: grouped ncclSend/ncclRecv over xGMI)"
         cap = rs.default_capacity(n)
         out = rs.empty_u32(cap, dev)
         vout = rs.empty_u32(cap, dev) if a.pairs else None
@@ -385,6 +475,7 @@ def main():
         import multi
         ops = multi.GpuOps(dev)
         res = {}
+        transport = "torch.distributed all_to_all (multi.py)" + (" over gloo (rehearsal)" if rehearsal else " over RCCL")
 
         def step():
             res["out"] = multi.dist_sort(keys, a.k, vals=vals, ops=ops)
@@ -420,13 +511,26 @@ def main():
     elapsed = float(el.item())
     # per-phase HIP events in a second, separate set of steps: the event records between the
     # phases cost ~10 us each (~85 us per C3 sort, rocprofv3 kernel trace), so `value` is timed
-    # without them and the roofline's per-launch kernel times come from these steps
+    # without them and the roofline's per-launch kernel times come from these steps; the multi-GPU
+    # sort also records its own phase boundaries there (rsort_multi_set_profiling)
+    multi_stats = []
+    prof_c = use_dist and a.dist_impl == "c"
     barrier()
-    with rs.Profile() as prof:
-        for _ in range(a.steps):
-            step()
-        torch.cuda.synchronize()
+    if prof_c:
+        rs.multi_set_profiling(True)
+    try:
+        with rs.Profile() as prof:
+            for _ in range(a.steps):
+                step()
+                if prof_c:
+                    multi_stats.append(rs.multi_last_stats())
+            torch.cuda.synchronize()
+    finally:
+        if prof_c:
+            rs.multi_set_profiling(False)
     barrier()
+    if prof_c and comm is not None and not rehearsal:
+        rccl_world = int(multi_stats[-1]["world"])  # rsort_u32_multi takes it from ncclCommCount
 
     # the timed output, checked on the device: sorted, same (key, value) multiset as the input
     # (summed over ranks for the multi-GPU step: each rank's slice is sorted, and the slices are
@@ -452,6 +556,10 @@ def main():
         ordered = all(nonempty[i][5] <= nonempty[i + 1][4] for i in range(len(nonempty) - 1))
         verified = (fin == fout and sum(x[2] for x in parts) == 0 and ordered
                     and sum(x[3] for x in parts) == n * world)
+        per_rank_stats = [multi_stats]
+        if world > 1 and prof_c:
+            per_rank_stats = [None] * world
+            dist.all_gather_object(per_rank_stats, multi_stats)
     else:
         fp_out, desc = rs.fingerprint(out, vout)
         verified = fp_out == fp_in and desc == 0
@@ -459,7 +567,8 @@ def main():
     kernels_used = rs.scatter_kernels_used(reset=True)  # what the dispatch launched in these steps
     probe = rs.lane_order_probe()
 
-    # per-kernel: the fused local-sort + scatter pass (the dominant kernel)
+    # per-kernel: the fused local-sort + scatter pass (the dominant kernel); in the multi-GPU step
+    # the partition's scatter is recorded apart (phase "partition") and the sample sort not at all
     sc = prof.times["scatter"]
     hi = prof.times["histogram"]
     scan = prof.times["scan"]
@@ -467,12 +576,12 @@ def main():
     scatter_ms = sc["ms"] / max(1, sc["launches"])
     keys_per_launch = sc["keys"] / max(1, sc["launches"])
     algo_bytes = bytes_per_key * keys_per_launch
-    achieved = algo_bytes / (scatter_ms * 1e-3) / 1e9
+    achieved = algo_bytes / (scatter_ms * 1e-3) / 1e9 if scatter_ms > 0 else 0.0
     # the pass's working kernel: the plain variant where a clustered-input twin (the same name ending
-    # in ", 1>" instead of ", 0>") was launched beside it
-    plain = [k for k in kernels_used if not (k.endswith(", 1>") and k[:-2] + "0>" in kernels_used)]
-    kernel = (plain[-1] if plain else rs.scatter_kernel_name(p)) if not use_dist else \
-        "rs_scatter_lines (partition and sort passes)"
+    # in ", 1>" instead of ", 0>") was launched beside it; never a partition instance
+    sort_kernels = [k for k in kernels_used if not is_partition_kernel(k)]
+    plain = [k for k in sort_kernels if not (k.endswith(", 1>") and k[:-2] + "0>" in sort_kernels)]
+    kernel = plain[-1] if plain else rs.scatter_kernel_name(p)
     cfg_key = f"n{n}_k{a.k}_{a.dist}_{'pairs' if a.pairs else 'keys'}_{a.rank}:{kernel.split('<')[0]}"
     prec, prec_src = profile_record(cfg_key) if not use_dist else (None, None)
 
@@ -494,9 +603,9 @@ def main():
 
     host_keys = None
     e2e = None
-    if rank == 0 and not use_dist and ((not a.no_cpu) or not a.no_e2e):
-        host_keys = rs.to_numpy_u32(keys)
-    if host_keys is not None and not a.no_e2e and not a.pairs:
+    if rank == 0 and ((not a.no_cpu) or (not a.no_e2e and not use_dist)):
+        host_keys = rs.to_numpy_u32(keys)  # (rank 0's own input keys in the multi-GPU step)
+    if host_keys is not None and not a.no_e2e and not a.pairs and not use_dist:
         # the reference's timing of sort(..., SORT_BY_DEVICE): device malloc + H2D + sort + D2H of
         # pageable host buffers (Parallel7.cu:646-661), through rsort_u32_ex; PCIe-bound, not `value`
         hout = np.empty_like(host_keys)
@@ -517,9 +626,15 @@ def main():
         for name in [x.strip() for x in a.configs.split(",") if x.strip()]:
             configs[name] = run_config(name, CONFIGS[name], dev, a.configs_reps, a.configs_n)
 
+    cpu = None
+    if rank == 0 and host_keys is not None and not a.no_cpu:
+        rows = [int(x) for x in a.cpu_rows.split(",") if x.strip()]
+        cpu = cpu_baseline(host_keys, min(a.cpu_n, n), a.k, a.cpu_reps, a.dist, rows)
+
     if rank == 0:
         total_keys = n * world * a.steps
-        roof = {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter)",
+        roof = {"bound": "hbm", "kernel": f"{kernel} (fused local sort + rank + scatter"
+                                          f"{'; the local sort after the exchange' if use_dist else ''})",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": prec["hbm_bytes_per_launch"] if prec else None,
@@ -533,6 +648,11 @@ def main():
             roof["avg_launch_ms_rocprof"] = round(rp, 4)
             roof["frac_rocprof"] = round(algo_bytes / (rp * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             roof["rocprof_source"] = prec.get("rocprof_source")
+            if prec.get("rocprof_csv_avg_ns"):
+                rc = prec["rocprof_csv_avg_ns"] * 1e-6
+                roof["avg_launch_ms_rocprof_csv"] = round(rc, 4)
+                roof["frac_rocprof_csv"] = round(algo_bytes / (rc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                roof["rocprof_csv_source"] = prec.get("rocprof_csv_source")
         line = {
             "metric": "Mkeys/s sorting 2^30 uniform uint32; scatter-pass achieved HBM GB/s",
             "value": round(total_keys / elapsed / 1e6, 1),
@@ -549,7 +669,9 @@ def main():
                      "zipf": "synthetic (Zipf s=1.0 over 2^20 ranks, key=fmix32(rank))",
                      "equal": "synthetic (every key 0x01234567)"}[a.dist],
             "config": {"workload": f"sort {n} {'key+value pairs' if a.pairs else 'uint32 keys'} per GPU, "
-                                   f"k={a.k} ({p.passes} passes), {a.dist}",
+                                   f"k={a.k} ({p.passes} passes), {a.dist}"
+                                   + (f"; {world} ranks, key-range partition + one exchange + local sort"
+                                      if use_dist else ""),
                        "keys_per_gpu": n, "k_bits": a.k, "passes": p.passes, "dist": a.dist,
                        "pairs": bool(a.pairs), "rank_algo": a.rank, "tile_keys": p.tile_keys,
                        "tiles_per_chunk": p.tiles_per_chunk, "num_chunks": p.num_chunks,
@@ -567,7 +689,7 @@ def main():
                                    else "wave64 ballot peer match (kRankCount)" if a.rank == "match"
                                    else "k 1-bit splits (kRankSplit)"),
                        "parallelism": "single GPU" if not use_dist else
-                       f"range-partition x{world} ({'rsort_u32_multi, RCCL send/recv' if a.dist_impl == 'c' else 'multi.py, torch all_to_all'}"
+                       f"range-partition x{world} ({transport}"
                        f"{', overlap' if a.dist_overlap and a.dist_impl == 'c' else ''}"
                        f"{', full protocol' if a.dist_full and a.dist_impl == 'c' else ''})"},
             "verified": bool(verified),
@@ -575,17 +697,22 @@ def main():
             "phases_ms_per_step": {"histogram": round(hi["ms"] / a.steps, 4), "scan": round(scan["ms"] / a.steps, 4),
                                    "scatter": round(sc["ms"] / a.steps, 4)},
         }
+        if use_dist and prof_c:
+            line["multi"] = multi_summary(per_rank_stats, world, {"rccl_world": rccl_world}, transport, sc,
+                                          prof.times["partition"])
         if configs:
             line["configs"] = configs
         if vendor:
             line["vendor"] = vendor
         if e2e:
             line["end_to_end"] = e2e
-        if host_keys is not None and not a.no_cpu:
-            rows = [int(x) for x in a.cpu_rows.split(",") if x.strip()]
-            line["cpu_baseline"] = cpu_baseline(host_keys, min(a.cpu_n, n), a.k, a.cpu_reps, a.dist, rows)
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
-    if comm is not None:
+    if host_tr is not None:
+        barrier()
+        host_tr.close()
+    if comm is not None and host_tr is None:
         comm.close()
     if use_dist:
         dist.destroy_process_group()

@@ -54,6 +54,7 @@ struct Profiler {
     }
 };
 Profiler g_prof;
+thread_local int t_prof_paused = 0;  // profile_pause
 
 // RAII scope: records a start event now and a stop event on destruction (same stream).
 struct PhaseScope {
@@ -61,6 +62,7 @@ struct PhaseScope {
     ProfRec rec{};
     hipStream_t s;
     PhaseScope(int phase, int64_t keys, hipStream_t stream) : s(stream) {
+        if (t_prof_paused > 0) return;
         std::lock_guard<std::mutex> g(g_prof.mu);
         if (!g_prof.on) return;
         rec.phase = phase;
@@ -83,9 +85,12 @@ int hip_status(hipError_t e) { return e == hipSuccess ? RSORT_OK : RSORT_ERR_HIP
 bool aligned4(const void *p) { return ((uintptr_t)p & 3u) == 0; }
 
 // The whole-line scatter kernels can write these outputs: any 4-B-aligned kout (launch_scatter
-// counts positions from its 128-B-aligned base); values at a multiple of 16 B from the keys.
-bool line_capable(const void *kout, const void *vout, int pairs) {
+// counts positions from its 128-B-aligned base, i.e. every position moves up by the < 32 keys
+// between that base and kout -- so n plus that shift must still fit the kernels' 32-bit positions);
+// values at a multiple of 16 B from the keys.
+bool line_capable(const void *kout, const void *vout, int pairs, int64_t n) {
     if (!aligned4(kout)) return false;
+    if (n + (int64_t)(((uintptr_t)kout & 127u) / 4u) >= ((int64_t)1 << 32)) return false;
     return !pairs || ((((uintptr_t)vout - (uintptr_t)kout) & 15u) == 0);
 }
 
@@ -353,10 +358,11 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     const int rank = internal_rank((dmode == kDigitShift) ? g_rank_algo.load() : RSORT_RANK_MATCH);
     const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
-    const int aligned16 = line_capable(kout, vout, p.pairs);
+    const int aligned16 = line_capable(kout, vout, p.pairs, p.n);
     if ((bounds || next_table) && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
         return RSORT_ERR_ARG;  // group chunks, next-digit counts: rs_scatter_lines only
-    PhaseScope ps(RSORT_PHASE_SCATTER, p.n, s);
+    // a multi-GPU partition's scatter (splitter digits) is recorded apart from the sort's passes
+    PhaseScope ps(dmode == kDigitSplit ? RSORT_PHASE_PARTITION : RSORT_PHASE_SCATTER, p.n, s);
     return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, local_only ? 0 : aligned16, a, s));
 }
 
@@ -400,14 +406,14 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // digit-group chunks on every second pass (joint_plan): needs rs_scatter_lines for both
     // outputs (lane-ordered ranks, 16-B aligned ping-pong buffers)
     const bool joint = joint_plan(p) && g_group_chunks.load() != 0 &&
-                       internal_rank(g_rank_algo.load()) == kRankAtomic && line_capable(kout, vout, p.pairs) &&
-                       line_capable(c.tmp_k, c.tmp_v, p.pairs);
+                       internal_rank(g_rank_algo.load()) == kRankAtomic && line_capable(kout, vout, p.pairs, p.n) &&
+                       line_capable(c.tmp_k, c.tmp_v, p.pairs, p.n);
     if (joint_plan(p) && !joint &&
         hipMemsetAsync(c.bounds, 0, (size_t)2 * kBoundsWords * 4, s) != hipSuccess)  // rsort_group_flags: none
         return RSORT_ERR_HIP;
     // next-digit counts (k = 3, 4): the same kernel conditions as digit groups
     const bool nextc = next_plan(p) && g_group_chunks.load() != 0 && internal_rank(g_rank_algo.load()) == kRankAtomic &&
-                       line_capable(kout, nullptr, 0) && line_capable(c.tmp_k, nullptr, 0);
+                       line_capable(kout, nullptr, 0, p.n) && line_capable(c.tmp_k, nullptr, 0, p.n);
     if (next_plan(p) && !nextc && hipMemsetAsync(c.done, 0, 8, s) != hipSuccess)  // rsort_plan_check: clean
         return RSORT_ERR_HIP;
     for (int i = 0; i < P; ++i) {
@@ -526,6 +532,8 @@ int host_sort(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t
 }
 
 }  // namespace
+
+void rsort::profile_pause(int delta) { t_prof_paused += delta; }
 
 // ================================================================================ C ABI
 extern "C" {

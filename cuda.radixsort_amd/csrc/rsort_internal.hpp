@@ -200,6 +200,9 @@ int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmod
 // Names of the scatter kernel instantiations launched since the last reset, ';'-joined into buf
 // (truncated to len - 1 characters); returns the full length. reset != 0 clears the record.
 size_t scatter_kernels_used(char *buf, size_t len, int reset);
+// rsort_profile_*: while a thread's pause count is > 0 its launches record no phase events (the
+// multi-GPU sort's sample sort, which is part of its plan phase, not of the measured passes)
+void profile_pause(int delta);
 // Workspace check words (next-digit plans): done[kDoneErr] is set when a tail scan found a table
 // whose total is not n even after an agent-scope acquire and a second sweep.
 constexpr uint32_t kDoneErr = 1;

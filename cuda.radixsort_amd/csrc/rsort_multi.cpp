@@ -44,6 +44,62 @@ constexpr int64_t kSampleBudget = (int64_t)1 << 20;
 constexpr int64_t kMaxPiece = (int64_t)1 << 28;
 std::atomic<int64_t> g_piece{kMaxPiece};  // rsort_set_exchange_piece (tests force several rounds)
 std::atomic<int> g_multi_opts{0};         // rsort_set_multi_options
+std::atomic<int> g_multi_prof{0};         // rsort_multi_set_profiling
+std::atomic<int> g_fail_rank{-1}, g_fail_stage{0}, g_fail_status{0};  // rsort_multi_inject_failure (tests)
+int injected(int rank, int stage) {
+    return (g_fail_rank.load() == rank && g_fail_stage.load() == stage) ? g_fail_status.load() : RSORT_OK;
+}
+// the calling thread's last profiled multi-GPU sort (the loopback tests run one rank per thread)
+thread_local rsort_multi_stats t_stats;
+thread_local bool t_stats_valid = false;
+
+// hipEvents at the phase boundaries of one multi-GPU sort, on the caller's stream (profiling only)
+struct MultiTimer {
+    enum { kStart, kPlan, kPartition, kExchange, kEnd, kMarks };
+    bool on = false;
+    hipStream_t s;
+    hipEvent_t ev[kMarks] = {};
+    bool marked[kMarks] = {};
+    MultiTimer(bool enable, hipStream_t stream) : s(stream) {
+        if (!enable) return;
+        on = true;
+        for (auto &e : ev)
+            if (hipEventCreate(&e) != hipSuccess) {
+                e = nullptr;
+                on = false;
+            }
+    }
+    ~MultiTimer() {
+        for (auto e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    void mark(int i) {
+        if (on && hipEventRecord(ev[i], s) == hipSuccess) marked[i] = true;
+    }
+    double ms(int a, int b) const {
+        float t = 0.f;
+        if (!marked[a] || !marked[b] || hipEventElapsedTime(&t, ev[a], ev[b]) != hipSuccess) return 0.0;
+        return t;
+    }
+    // waits for the sort to finish (profiling makes the call synchronous) and keeps the record
+    int finish(rsort_multi_stats &st) {
+        if (!on) return RSORT_OK;
+        mark(kEnd);
+        if (hipEventSynchronize(ev[kEnd]) != hipSuccess) return RSORT_ERR_HIP;
+        // phases without a mark of their own (the direct world-1 sort) take the time up to the next
+        int prev = kStart;
+        double *out[kMarks] = {nullptr, &st.ms_plan, &st.ms_partition, &st.ms_exchange, &st.ms_local_sort};
+        for (int i = kPlan; i < kMarks; ++i) {
+            if (!marked[i]) continue;
+            *out[i] = ms(prev, i);
+            prev = i;
+        }
+        st.ms_total = ms(kStart, kEnd);
+        t_stats = st;
+        t_stats_valid = true;
+        return RSORT_OK;
+    }
+};
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -267,6 +323,57 @@ int lb_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void *
     return st;
 }
 
+// ------------------------------------------------------------------------------ host transport
+// rsort_host_transport_wrap: device bytes staged through host buffers for a host-memory transport
+struct HostCtx {
+    rsort_host_transport host;
+    std::vector<char> send, recv;
+};
+
+int host_allgather(void *ctx, const void *d_send, void *d_recv, size_t bytes, void *stream) {
+    HostCtx *c = static_cast<HostCtx *>(ctx);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t world = (size_t)c->host.world;
+    c->send.resize(std::max<size_t>(bytes, 1));
+    c->recv.resize(std::max<size_t>(world * bytes, 1));
+    if (bytes && hipMemcpyAsync(c->send.data(), d_send, bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    const int st = c->host.allgather(c->host.ctx, c->send.data(), c->recv.data(), bytes);
+    if (st) return st;
+    if (bytes && hipMemcpyAsync(d_recv, c->recv.data(), world * bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    return hip_st(hipStreamSynchronize(s));
+}
+
+int host_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void *const *d_recv,
+                  const size_t *recv_bytes, void *stream) {
+    HostCtx *c = static_cast<HostCtx *>(ctx);
+    hipStream_t s = (hipStream_t)stream;
+    const int world = c->host.world;
+    size_t so[kMaxRanks + 1] = {0}, ro[kMaxRanks + 1] = {0};
+    for (int p = 0; p < world; ++p) {
+        so[p + 1] = so[p] + send_bytes[p];
+        ro[p + 1] = ro[p] + recv_bytes[p];
+    }
+    c->send.resize(std::max<size_t>(so[world], 1));
+    c->recv.resize(std::max<size_t>(ro[world], 1));
+    void *hs[kMaxRanks], *hr[kMaxRanks];
+    for (int p = 0; p < world; ++p) {
+        hs[p] = c->send.data() + so[p];
+        hr[p] = c->recv.data() + ro[p];
+        if (send_bytes[p] && hipMemcpyAsync(hs[p], d_send[p], send_bytes[p], hipMemcpyDeviceToHost, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    const int st = c->host.exchange(c->host.ctx, hs, send_bytes, hr, recv_bytes);
+    if (st) return st;
+    for (int p = 0; p < world; ++p)
+        if (recv_bytes[p] && hipMemcpyAsync(d_recv[p], hr[p], recv_bytes[p], hipMemcpyHostToDevice, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+    return hip_st(hipStreamSynchronize(s));
+}
+
 // ------------------------------------------------------------------------------ the sort
 int d2h(void *h, const void *d, size_t bytes, hipStream_t s) {
     if (hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return RSORT_ERR_HIP;
@@ -299,6 +406,14 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     if (local != RSORT_OK) n = 0;  // (nothing below reads the keys of a failed rank)
     int st;
     const int opts = g_multi_opts.load();
+    rsort_multi_stats stats;
+    memset(&stats, 0, sizeof(stats));
+    stats.world = world;
+    stats.rank = me;
+    stats.n_in = n;
+    stats.bytes_per_key = pairs ? 8 : 4;
+    MultiTimer timer(g_multi_prof.load() != 0, s);
+    timer.mark(MultiTimer::kStart);
     if (world == 1 && !(opts & RSORT_MULTI_FULL)) {
         // one rank: the partition would be one bucket (a copy) and the exchange a self copy, so the
         // keys go straight through the local sort (same output, no peers to agree with)
@@ -311,7 +426,12 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         }
         *out_n = n;
         *out_offset = 0;
-        return RSORT_OK;
+        stats.direct = 1;
+        stats.halves = 1;
+        stats.n_out = n;
+        stats.send_keys[0] = stats.recv_keys[0] = n;
+        timer.mark(MultiTimer::kExchange);  // (nothing exchanged: the whole time is the local sort)
+        return timer.finish(stats);
     }
     // RSORT_MULTI_OVERLAP: every rank's key range is cut in two (H = 2 virtual ranks per rank, the
     // planning functions run for world * H ranks); the lower half is exchanged first and sorted on a
@@ -370,40 +490,58 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         // the rows (each followed by its status word) sorted as one array: the status words are 0
         // and sort first, so the quantile positions move up by world
         const int64_t ns = (int64_t)world * (int64_t)row;
+        profile_pause(1);  // (its passes are part of the plan phase, not the measured local sort)
         local = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s);
+        profile_pause(-1);
         for (int i = 1; i < V && !local; ++i)
             if (hipMemcpyAsync(&q[i - 1], m.samp_all + world + rsort_multi_quantile_index(&sp, i), 4,
                                hipMemcpyDeviceToHost, s) != hipSuccess)
                 local = RSORT_ERR_HIP;
         if (!local && hipStreamSynchronize(s) != hipSuccess) local = RSORT_ERR_HIP;
+        if (!local) local = injected(me, 1);
+        if (local) q[0] = 0xFFFFFFFFu;  // (a failed copy may leave partial quantiles: replaced below)
     }
+    // From here a rank that failed since the last status exchange (the sample sort, a quantile copy)
+    // still joins the next all-gather with a row of the same size as its peers' and its status in
+    // it: it plans on placeholder quantiles (all 0, monotone) instead of its partial ones, and a
+    // failure of the pure splitter planning is carried the same way instead of returned.
+    if (local) memset(q, 0, sizeof(q));
     rsort_multi_splitters spl;
-    if ((st = rsort_multi_splitters_make(V, q, &spl))) return st;  // pure, identical on every rank
+    if ((st = rsort_multi_splitters_make(V, q, &spl))) {  // pure, identical on every healthy rank
+        if (!local) local = st;
+        memset(&spl, 0, sizeof(spl));
+        spl.world = V;
+    }
+    timer.mark(MultiTimer::kPlan);
 
     // 3. stable partition into the splitters' buckets
-    const int buckets = spl.nsplit + 1;
-    if (buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;  // pure: the same on every rank
+    const int buckets = std::min(spl.nsplit + 1, kMaxSplitters + 1);
+    if (spl.nsplit + 1 > kMaxSplitters + 1 && !local) local = RSORT_ERR_ARG;  // (pure: every rank alike)
     uint32_t starts[kMaxBuckets + 1] = {0};
+    if (!local) local = injected(me, 2);
     if (!local)
         local = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, spl.split, buckets, m.starts, m.sub,
                                        m.sub_bytes, s);
     if (!local) local = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s);
 
-    // 4. count matrix + capacities + statuses -> the exchange plans (the same on every rank)
-    uint64_t rowc[kMaxBuckets + 2];
-    for (int b = 0; b < buckets; ++b) rowc[b] = local ? 0u : (uint64_t)(starts[b + 1] - starts[b]);
-    rowc[buckets] = (uint64_t)capacity;
-    rowc[buckets + 1] = (uint64_t)local;
-    const size_t row_bytes = (size_t)(buckets + 2) * 8;
+    // 4. count matrix + capacities + statuses -> the exchange plans (the same on every rank). The
+    //    row has a fixed size whatever this rank's bucket count (a failed rank's may differ), so the
+    //    all-gather always matches: counts in [0, buckets), capacity and status at fixed words.
+    constexpr int kRow = kMaxBuckets + 2, kCapWord = kMaxBuckets, kStatusWord = kMaxBuckets + 1;
+    uint64_t rowc[kRow] = {0};
+    for (int b = 0; b < buckets && !local; ++b) rowc[b] = (uint64_t)(starts[b + 1] - starts[b]);
+    rowc[kCapWord] = (uint64_t)capacity;
+    rowc[kStatusWord] = (uint64_t)local;
+    const size_t row_bytes = sizeof(rowc);
     if (hipMemcpyAsync(m.c_send, rowc, row_bytes, hipMemcpyHostToDevice, s) != hipSuccess) return RSORT_ERR_HIP;
     if ((st = tr->allgather(tr->ctx, m.c_send, m.c_all, row_bytes, s))) return st;
-    uint64_t all[kMaxRanks * (kMaxBuckets + 2)];
+    uint64_t all[kMaxRanks * kRow];
     if ((st = d2h(all, m.c_all, (size_t)world * row_bytes, s))) return st;
-    if ((st = first_status(all, (size_t)buckets + 2, (size_t)buckets + 1))) return st;
+    if ((st = first_status(all, (size_t)kRow, (size_t)kStatusWord))) return st;
     int64_t counts[kMaxRanks * kMaxBuckets] = {0}, caps[kMaxRanks], cap_of[kMaxRanks];
     for (int r = 0; r < world; ++r) {
-        for (int b = 0; b < buckets; ++b) counts[r * H * buckets + b] = (int64_t)all[r * (buckets + 2) + b];
-        cap_of[r] = (int64_t)all[r * (buckets + 2) + buckets];
+        for (int b = 0; b < buckets; ++b) counts[r * H * buckets + b] = (int64_t)all[r * kRow + b];
+        cap_of[r] = (int64_t)all[r * kRow + kCapWord];
         for (int h = 0; h < H; ++h) caps[r * H + h] = cap_of[r];  // (the halves' sum is checked below)
     }
     // every virtual rank's plan: this rank sends as virtual rank me * H and receives as me * H + h;
@@ -426,13 +564,30 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     //      sort runs on the side stream while the second half is exchanged.
     int64_t rounds = 0, piece = 0;
     if ((st = rsort_multi_exchange_rounds(xs.max_message, g_piece.load(), &rounds, &piece))) return st;
+    timer.mark(MultiTimer::kPartition);
+    stats.halves = H;
+    stats.rounds = rounds;
+    for (int p = 0; p < world; ++p)
+        for (int h = 0; h < H; ++h) {
+            stats.send_keys[p] += xs.send_cnt[p * H + h];
+            stats.recv_keys[p] += xv[me * H + h].recv_cnt[p * H];
+        }
     SideStream *side = side_stream();
+    // On EVERY return while the side stream holds work (an own-range copy, the lower half's sort)
+    // `s` first waits for it, so a caller that synchronises `s` after an error never frees buffers
+    // a side-stream kernel still writes; only then does the stream go back to the pool (a later user
+    // enqueues behind the work anyway, and the wait already captured the event's state).
     struct SideGuard {
         SideStream *x;
-        ~SideGuard() { side_release(x); }  // (waits already enqueued keep the events' state)
-    } side_guard{side};
+        hipStream_t s;
+        bool pending = false;  // the side stream holds work `s` must wait for
+        ~SideGuard() {
+            if (x && pending) (void)hipStreamWaitEvent(s, x->done, 0);
+            side_release(x);
+        }
+    } side_guard{side, s};
+    bool &side_pending = side_guard.pending;
     int64_t base = 0;
-    bool side_pending = false;  // the side stream holds work `s` must wait for
     for (int h = 0; h < H; ++h) {
         const rsort_exchange_plan &xd = xv[me * H + h];
         const int own_dst = me * H + h, own_src = me * H;
@@ -473,11 +628,14 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
                 if ((st = tr->exchange(tr->ctx, sp_, sb, rp_, rb, s))) return st;
             }
         }
-        // this half has arrived (on `s`, and its own range on the side stream)
+        // this half has arrived (on `s`, and its own range on the side stream); under the overlap the
+        // exchange phase ends with the last message, before waiting for the lower half's sort
+        if (h + 1 == H && H > 1) timer.mark(MultiTimer::kExchange);
         if (side_pending) {
             if (hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
             side_pending = false;
         }
+        if (h + 1 == H && H == 1) timer.mark(MultiTimer::kExchange);
         if (xd.n_recv > 0) {
             rsort_plan p;
             if ((st = rsort_plan_make(xd.n_recv, k_bits, pairs, 0, &p))) return st;
@@ -493,10 +651,14 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         }
         base += xd.n_recv;
     }
-    if (side_pending && hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
+    if (side_pending) {
+        if (hipStreamWaitEvent(s, side->done, 0) != hipSuccess) return RSORT_ERR_HIP;
+        side_pending = false;
+    }
     *out_n = base;
     *out_offset = xv[me * H].offset;
-    return RSORT_OK;
+    stats.n_out = base;
+    return timer.finish(stats);
 }
 
 }  // namespace
@@ -529,6 +691,27 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
                       d_workspace, workspace_bytes, (hipStream_t)stream);
 }
 
+int rsort_multi_inject_failure(int rank, int stage, int status) {
+    if (rank < 0) {
+        g_fail_rank.store(-1);
+        g_fail_stage.store(0);
+        return RSORT_OK;
+    }
+    if (stage < 1 || stage > 2 || status == RSORT_OK) return RSORT_ERR_ARG;
+    g_fail_status.store(status);
+    g_fail_stage.store(stage);
+    g_fail_rank.store(rank);
+    return RSORT_OK;
+}
+
+int rsort_multi_set_profiling(int enable) { return g_multi_prof.exchange(enable ? 1 : 0); }
+
+int rsort_multi_last_stats(rsort_multi_stats *out) {
+    if (!out || !t_stats_valid) return RSORT_ERR_ARG;
+    *out = t_stats;
+    return RSORT_OK;
+}
+
 int rsort_set_multi_options(int flags) {
     return g_multi_opts.exchange(flags & (RSORT_MULTI_OVERLAP | RSORT_MULTI_FULL));
 }
@@ -537,6 +720,23 @@ int64_t rsort_set_exchange_piece(int64_t keys) {
     const int64_t old = g_piece.load();
     if (keys >= 64 && keys <= kMaxPiece) g_piece.store(keys);
     return old;
+}
+
+int rsort_host_transport_wrap(const rsort_host_transport *host, rsort_transport *out) {
+    if (!host || !out || !host->allgather || !host->exchange || host->world < 1 || host->world > kMaxRanks ||
+        host->rank < 0 || host->rank >= host->world)
+        return RSORT_ERR_ARG;
+    HostCtx *c = new (std::nothrow) HostCtx();
+    if (!c) return RSORT_ERR_ALLOC;
+    c->host = *host;
+    *out = rsort_transport{c, host->world, host->rank, host_allgather, host_exchange};
+    return RSORT_OK;
+}
+
+void rsort_host_transport_free(rsort_transport *wrapped) {
+    if (!wrapped || wrapped->allgather != host_allgather) return;
+    delete static_cast<HostCtx *>(wrapped->ctx);
+    wrapped->ctx = nullptr;
 }
 
 int rsort_loopback_create(int world, void **group) {

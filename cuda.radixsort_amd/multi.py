@@ -79,6 +79,32 @@ class GpuOps:
         return keys, vals
 
 
+def host_transport(group=None) -> "rs.HostTransport":
+    """The C multi-GPU sort (rsort_u32_multi_transport) over a torch.distributed group whose
+    collectives run on HOST tensors (gloo): rsort_host_transport_wrap stages the device bytes, these
+    callbacks move them. For rehearsing the N-rank C protocol with several ranks on one card (RCCL
+    refuses two ranks on one GPU) and in CPU-side tests; the product path on a node is RCCL."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+
+    def allgather(send):
+        t = torch.from_numpy(send)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return torch.cat(out).numpy().tobytes()
+
+    def exchange(sends, recv_sizes):
+        inp = torch.from_numpy(np.concatenate(sends) if sends else np.empty(0, np.uint8))
+        out = torch.empty(sum(recv_sizes), dtype=torch.uint8)
+        dist.all_to_all_single(out, inp, output_split_sizes=list(recv_sizes),
+                               input_split_sizes=[int(x.size) for x in sends], group=group)
+        o = out.numpy()
+        offs = np.concatenate([[0], np.cumsum(recv_sizes)]).astype(np.int64)
+        return [o[offs[p]:offs[p + 1]].tobytes() for p in range(world)]
+
+    return rs.HostTransport(world, rank, allgather, exchange)
+
+
 def exchange_rounds(max_message: int, limit: int) -> tuple[int, int]:
     """(rounds, piece) for messages of up to max_message keys, <= limit keys each: the C planning
     function rsort_multi_exchange_rounds (pieces a multiple of 64 keys, rounded down)."""

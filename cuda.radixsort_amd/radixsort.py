@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import enum
+import os
 import time
 from contextlib import contextmanager
 from pathlib import Path
@@ -40,7 +41,7 @@ STATUS_NAMES = {0: "RSORT_OK", 1: "RSORT_ERR_ARG", 2: "RSORT_ERR_BITS", 3: "RSOR
                 7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV", 9: "RSORT_ERR_CAPACITY",
                 10: "RSORT_ERR_COMM"}
 RANK_MATCH, RANK_SPLIT, RANK_BALLOT = 0, 1, 2
-PHASES = ("histogram", "scan", "scatter", "copy")
+PHASES = ("histogram", "scan", "scatter", "copy", "partition")
 
 
 class Implementation(enum.IntEnum):
@@ -74,7 +75,8 @@ class Plan(ctypes.Structure):
 
 
 class PhaseTimes(ctypes.Structure):
-    _fields_ = [("ms", ctypes.c_double * 4), ("launches", ctypes.c_int64 * 4), ("keys", ctypes.c_int64 * 4)]
+    _fields_ = [("ms", ctypes.c_double * len(PHASES)), ("launches", ctypes.c_int64 * len(PHASES)),
+                ("keys", ctypes.c_int64 * len(PHASES))]
 
     def as_dict(self):
         return {p: {"ms": self.ms[i], "launches": self.launches[i], "keys": self.keys[i]}
@@ -121,6 +123,35 @@ class Transport(ctypes.Structure):
     """rsort_transport: the multi-GPU sort's communication plug-in."""
     _fields_ = [("ctx", ctypes.c_void_p), ("world", ctypes.c_int32), ("rank", ctypes.c_int32),
                 ("allgather", _AG_FN), ("exchange", _EX_FN)]
+
+
+_HAG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_HEX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                           ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_void_p),
+                           ctypes.POINTER(ctypes.c_size_t))
+
+
+class HostTransportFns(ctypes.Structure):
+    """rsort_host_transport: a transport over host memory (wrapped by rsort_host_transport_wrap)."""
+    _fields_ = [("ctx", ctypes.c_void_p), ("world", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("allgather", _HAG_FN), ("exchange", _HEX_FN)]
+
+
+class MultiStats(ctypes.Structure):
+    """rsort_multi_stats: the phases and traffic of one multi-GPU sort (rsort_multi_last_stats)."""
+    _fields_ = [("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("halves", ctypes.c_int32),
+                ("direct", ctypes.c_int32), ("rounds", ctypes.c_int64), ("bytes_per_key", ctypes.c_int64),
+                ("send_keys", ctypes.c_int64 * MAX_RANKS), ("recv_keys", ctypes.c_int64 * MAX_RANKS),
+                ("n_in", ctypes.c_int64), ("n_out", ctypes.c_int64),
+                ("ms_plan", ctypes.c_double), ("ms_partition", ctypes.c_double), ("ms_exchange", ctypes.c_double),
+                ("ms_local_sort", ctypes.c_double), ("ms_total", ctypes.c_double)]
+
+    def as_dict(self):
+        w = self.world
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("send_keys", "recv_keys")}
+        d["send_keys"] = [int(self.send_keys[i]) for i in range(w)]
+        d["recv_keys"] = [int(self.recv_keys[i]) for i in range(w)]
+        return d
 
 
 # Every symbol include/rsort.h declares, with its ctypes signature.
@@ -171,6 +202,11 @@ SIGNATURES = {
     "rsort_set_exchange_piece": ([_i64], _i64),
     "rsort_set_multi_options": ([_int], _int),
     "rsort_multi_exchange_rounds": ([_i64, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
+    "rsort_multi_set_profiling": ([_int], _int),
+    "rsort_multi_inject_failure": ([_int, _int, _int], _int),
+    "rsort_multi_last_stats": ([ctypes.POINTER(MultiStats)], _int),
+    "rsort_host_transport_wrap": ([ctypes.POINTER(HostTransportFns), ctypes.POINTER(Transport)], _int),
+    "rsort_host_transport_free": ([ctypes.POINTER(Transport)], None),
     "rsort_loopback_create": ([_int, ctypes.POINTER(ctypes.c_void_p)], _int),
     "rsort_loopback_transport": ([ctypes.c_void_p, _int, ctypes.POINTER(Transport)], _int),
     "rsort_loopback_destroy": ([ctypes.c_void_p], None),
@@ -399,7 +435,9 @@ def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
         ((p.threads, p.tile_keys) == (1024, 8192) and p.pairs and 5 <= p.k_bits <= 8) or \
         ((p.threads, p.tile_keys) == (256, 4096) and not p.pairs and 3 <= p.k_bits <= 4)
     if lines and out_aligned16 and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
-        return "rs_scatter_pairs" if p.pairs and p.k_bits >= 7 else "rs_scatter_lines"
+        # RSORT_PAIRS64=1 (A/B runs) makes the library's dispatch take the 64-B-line pairs kernel
+        pairs64 = os.environ.get("RSORT_PAIRS64", "") not in ("", "0")
+        return "rs_scatter_pairs" if p.pairs and p.k_bits >= 7 and not pairs64 else "rs_scatter_lines"
     return "rs_scatter"
 
 
@@ -501,6 +539,72 @@ def multi_options(flags: int):
 def set_exchange_piece(keys: int) -> int:
     """Largest exchange message per round of rsort_u32_multi* (keys); returns the old value."""
     return int(_lib().rsort_set_exchange_piece(int(keys)))
+
+
+def multi_set_profiling(enable: bool) -> bool:
+    """rsort_multi_set_profiling: per-phase hipEvents in every multi-GPU sort (which then syncs)."""
+    return bool(_lib().rsort_multi_set_profiling(1 if enable else 0))
+
+
+def multi_last_stats() -> dict:
+    """rsort_multi_last_stats: the calling thread's last profiled multi-GPU sort."""
+    st = MultiStats()
+    _check(_lib().rsort_multi_last_stats(ctypes.byref(st)), "rsort_multi_last_stats")
+    return st.as_dict()
+
+
+class HostTransport:
+    """rsort_host_transport_wrap over two Python callables working on host (numpy) buffers:
+    allgather(send: np.uint8 array) -> bytes-like of world * len(send) bytes in rank order, and
+    exchange(sends: list of np.uint8 arrays, recv_sizes: list of int) -> list of bytes-like. The
+    C wrapper stages the device bytes; `.transport` is the rsort_transport to pass as `comm`."""
+
+    def __init__(self, world: int, rank: int, allgather, exchange):
+        self.world, self.rank = world, rank
+        self._errors = []
+
+        def ag(ctx, h_send, h_recv, nbytes):
+            try:
+                send = np.ctypeslib.as_array((ctypes.c_uint8 * max(1, nbytes)).from_address(h_send))[:nbytes]
+                got = np.frombuffer(allgather(send.copy()), dtype=np.uint8)
+                if got.size != world * nbytes:
+                    raise ValueError(f"allgather returned {got.size} bytes, expected {world * nbytes}")
+                if got.size:
+                    ctypes.memmove(h_recv, got.ctypes.data, got.size)
+                return 0
+            except Exception as e:  # noqa: BLE001 -- any failure is a communication error to the C side
+                self._errors.append(e)
+                return 10  # RSORT_ERR_COMM
+
+        def ex(ctx, h_send, send_bytes, h_recv, recv_bytes):
+            try:
+                sends = [np.ctypeslib.as_array((ctypes.c_uint8 * send_bytes[p]).from_address(h_send[p])).copy()
+                         if send_bytes[p] else np.empty(0, np.uint8) for p in range(world)]
+                outs = exchange(sends, [int(recv_bytes[p]) for p in range(world)])
+                for p in range(world):
+                    o = np.frombuffer(outs[p], dtype=np.uint8)
+                    if o.size != recv_bytes[p]:
+                        raise ValueError(f"exchange: {o.size} bytes from rank {p}, expected {recv_bytes[p]}")
+                    if o.size:
+                        ctypes.memmove(h_recv[p], o.ctypes.data, o.size)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                self._errors.append(e)
+                return 10
+
+        self._fns = HostTransportFns(None, world, rank, _HAG_FN(ag), _HEX_FN(ex))  # keeps the callbacks alive
+        self.transport = Transport()
+        _check(_lib().rsort_host_transport_wrap(ctypes.byref(self._fns), ctypes.byref(self.transport)),
+               "rsort_host_transport_wrap")
+        self.transport.world, self.transport.rank = world, rank
+
+    @property
+    def errors(self):
+        return list(self._errors)
+
+    def close(self):
+        if self.transport.ctx:
+            _lib().rsort_host_transport_free(ctypes.byref(self.transport))
 
 
 class LoopbackGroup:

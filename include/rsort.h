@@ -81,7 +81,10 @@ typedef enum rsort_phase {
     RSORT_PHASE_SCAN = 1,
     RSORT_PHASE_SCATTER = 2, /* fused block-local sort + rank + scatter: the measured pass */
     RSORT_PHASE_COPY = 3,    /* device-to-device copies (in-place sorts with an odd pass count) */
-    RSORT_PHASE_COUNT = 4
+    RSORT_PHASE_PARTITION = 4, /* the multi-GPU key-range partition's scatter kernel (its histogram
+                                  and scan count as HISTOGRAM and SCAN), kept apart from the sort's
+                                  scatter passes so each has its own roofline figure */
+    RSORT_PHASE_COUNT = 5
 } rsort_phase;
 
 typedef struct rsort_phase_times {
@@ -337,6 +340,37 @@ RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, in
 #define RSORT_MULTI_FULL 2
 RSORT_API int rsort_set_multi_options(int flags);
 
+/* Per-phase record of a multi-GPU sort (rsort_u32_multi*), for the N-GPU bench line. Off by
+ * default; while on, every multi-GPU sort records hipEvents on its stream at the phase boundaries
+ * and synchronises its stream before returning (so it is no longer asynchronous), and the calling
+ * thread's last sort is kept for rsort_multi_last_stats. Phases on the caller's stream:
+ *   plan       count all-gather, sampling, sample all-gather + device sort, splitters
+ *   partition  the stable partition, the count/capacity all-gather, the exchange plan
+ *   exchange   every exchange round (and the own range's device copy beside it)
+ *   local_sort the LSD sort of what arrived
+ * With RSORT_MULTI_OVERLAP the lower half's sort runs on a second stream during the upper half's
+ * exchange: `exchange` then ends when the last message has arrived and `local_sort` is the rest. */
+typedef struct rsort_multi_stats {
+    int32_t world;       /* ranks of the communicator (rsort_u32_multi: ncclCommCount) */
+    int32_t rank;        /* this rank (rsort_u32_multi: ncclCommUserRank) */
+    int32_t halves;      /* 1, or 2 under RSORT_MULTI_OVERLAP */
+    int32_t direct;      /* 1: world 1 without RSORT_MULTI_FULL, sorted directly (phases: local_sort) */
+    int64_t rounds;      /* exchange rounds (messages per peer and array) */
+    int64_t bytes_per_key; /* 4 (keys) or 8 (key + value) */
+    int64_t send_keys[RSORT_MAX_RANKS]; /* keys this rank sent to each rank (own entry: the device copy) */
+    int64_t recv_keys[RSORT_MAX_RANKS]; /* keys it received from each rank */
+    int64_t n_in, n_out; /* keys in, keys out on this rank */
+    double ms_plan, ms_partition, ms_exchange, ms_local_sort, ms_total;
+} rsort_multi_stats;
+RSORT_API int rsort_multi_set_profiling(int enable); /* process-wide; returns the previous setting */
+/* The calling thread's last multi-GPU sort made while profiling was on (RSORT_ERR_ARG if none). */
+RSORT_API int rsort_multi_last_stats(rsort_multi_stats *out);
+
+/* TEST HOOK (fault injection for the error-agreement tests; never set in production): the next
+ * multi-GPU sorts of rank `rank` fail with `status` at `stage` (1: the sample sort, after the sample
+ * all-gather; 2: the partition), as a device failure there would. rank < 0 clears the hook. */
+RSORT_API int rsort_multi_inject_failure(int rank, int stage, int status);
+
 /* Largest message of one exchange round, in keys (default and maximum 2^28 = 1 GiB; >= 64).
  * Messages are cut into equal pieces of a multiple of 64 keys rounded DOWN, so no message exceeds
  * the limit even when it is not a multiple of 64. Process-wide; returns the previous value. Tests
@@ -362,6 +396,22 @@ RSORT_API int rsort_u32_multi_transport(const uint32_t *d_keys, const uint32_t *
                                         int64_t *out_n, int64_t *out_offset, int k_bits,
                                         const rsort_transport *transport, void *d_workspace,
                                         size_t workspace_bytes, void *stream);
+/* A transport over HOST memory (MPI, gloo, sockets, ...), wrapped into an rsort_transport: the
+ * wrapper synchronises the stream, stages the device bytes through host buffers it owns, calls
+ * the host functions (same contract as rsort_transport, host pointers) and copies the results back
+ * to the device. bench.py's N-rank rehearsal on one card and the gloo tests run the C protocol this
+ * way; the product path on a multi-GPU node is RCCL (rsort_u32_multi). The wrapper keeps a copy of
+ * *host; free it with rsort_host_transport_free after the last sort. */
+typedef struct rsort_host_transport {
+    void *ctx;
+    int32_t world, rank;
+    int (*allgather)(void *ctx, const void *h_send, void *h_recv, size_t bytes);
+    int (*exchange)(void *ctx, void *const *h_send, const size_t *send_bytes, void *const *h_recv,
+                    const size_t *recv_bytes);
+} rsort_host_transport;
+RSORT_API int rsort_host_transport_wrap(const rsort_host_transport *host, rsort_transport *out);
+RSORT_API void rsort_host_transport_free(rsort_transport *wrapped);
+
 /* In-process loopback world: `world` ranks, one host thread each, calling
  * rsort_u32_multi_transport concurrently on their own streams (one device, or devices with peer
  * access). Collectives are a host rendezvous plus device-to-device copies; a rank that waits more

@@ -73,3 +73,74 @@ def test_bench_pairs_zipf_verified():
     d = run_bench("--steps", "1", "--warmup", "1", "--keys", str(1 << 24), "--dist", "zipf", "--pairs", "--no-cpu",
                   "--configs", "")
     assert d["verified"] is True and d["config"]["pairs"] is True
+
+
+def run_bench_env(env_extra, *args, timeout=300):
+    import os
+    env = dict(os.environ)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=str(ROOT), env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout[-2000:], r.stderr[-2000:])
+    return json.loads(lines[0])
+
+
+def check_multi_block(d, world):
+    m = d["multi"]
+    assert m["transport_world"] == world and m["halves"] in (1, 2) and m["exchange_rounds"] >= 0
+    ph = m["phases_ms_per_step"]
+    for k in ("plan", "partition", "exchange", "local_sort", "total"):
+        assert ph[k] >= 0, k
+    assert ph["total"] > 0 and ph["local_sort"] > 0
+    assert len(m["phases_ms_per_rank"]) == world and len(m["keys_out_per_rank"]) == world
+    ex = m["exchange"]
+    assert len(ex["bytes_sent_per_rank"]) == world and len(ex["bytes_recv_per_rank"]) == world
+    # every key leaves its rank or stays in its own range: sent + own = the rank's input bytes
+    n = d["config"]["keys_per_gpu"]
+    for r in range(world):
+        assert ex["bytes_sent_per_rank"][r] + ex["own_range_bytes_per_rank"][r] == n * ex["bytes_per_key"]
+    assert sum(ex["bytes_sent_per_rank"]) == sum(ex["bytes_recv_per_rank"])
+    assert sum(m["keys_out_per_rank"]) == n * world
+    ls = m["local_sort_scatter"]
+    assert ls is not None and 0 < ls["frac"] < 1 and ls["avg_launch_ms"] > 0
+    # the top-level roofline is the local sort's scatter kernel, never a partition instance
+    sys.path.insert(0, str(ROOT))
+    from bench import is_partition_kernel
+    kernel = d["roofline"]["kernel"].split(" (")[0]
+    assert kernel.startswith("rs_scatter") and not is_partition_kernel(kernel), kernel
+    assert any(is_partition_kernel(k) for k in d["config"]["scatter_kernels"])
+    if world > 1:
+        assert m["partition_scatter"] is not None and m["partition_scatter"]["avg_launch_ms"] > 0
+
+
+def test_bench_plain_gpus2_self_launches_rehearsal():
+    """`python bench.py --gpus 2` started plainly (no torch.distributed.run, as the driver may):
+    bench.py starts the two ranks itself; RSORT_BENCH_BACKEND=gloo lets both share the one card
+    (the C protocol over a gloo host transport; RCCL refuses two ranks on one GPU)."""
+    d = run_bench_env({"RSORT_BENCH_BACKEND": "gloo"}, "--gpus", "2", "--steps", "2", "--warmup", "1",
+                      "--keys", str((1 << 22) + 333), "--cpu-n", str(1 << 18), "--cpu-reps", "1", "--cpu-rows", "")
+    assert d["n_gpus"] == 2 and d["verified"] is True and d["value"] > 0
+    assert "range-partition x2" in d["config"]["parallelism"] and "gloo" in d["config"]["parallelism"]
+    assert d["multi"]["rccl_world"] is None  # (no RCCL communicator in the rehearsal)
+    check_multi_block(d, 2)
+    assert d["multi"]["exchange"]["link_GBs"]["links"] == 2
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1
+
+
+def test_bench_gpus2_overlap_pairs_rehearsal():
+    d = run_bench_env({"RSORT_BENCH_BACKEND": "gloo"}, "--gpus", "2", "--steps", "1", "--warmup", "1",
+                      "--keys", str(1 << 21), "--dist", "zipf", "--pairs", "--dist-overlap", "--no-cpu")
+    assert d["n_gpus"] == 2 and d["verified"] is True
+    check_multi_block(d, 2)
+    assert d["multi"]["halves"] == 2 and d["multi"]["exchange"]["bytes_per_key"] == 8
+
+
+def test_bench_one_rank_rccl_reports_phases():
+    """One rank over RCCL, the whole protocol: rccl_world comes from ncclCommCount."""
+    d = run_bench_env({}, "--dist-path", "--dist-full", "--steps", "1", "--warmup", "1", "--keys", str(1 << 22),
+                      "--no-cpu")
+    assert d["verified"] is True and d["multi"]["rccl_world"] == 1
+    check_multi_block(d, 1)

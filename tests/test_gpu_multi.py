@@ -204,10 +204,11 @@ def _loopback_inputs(rank, n, dist_name, pairs):
     return keys, vals
 
 
-def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0):
+def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0, stats=None, transports=None):
     """world threads in this process, one stream each, calling rsort_u32_multi_transport with
-    the loopback transport on cuda:0 concurrently. Returns per-rank (keys, vals, offset) or the
-    per-rank RSortError statuses."""
+    the loopback transport (or `transports[r]`) on cuda:0 concurrently. Returns per-rank (keys, vals,
+    offset) or the per-rank RSortError statuses. stats: a list that receives every rank's
+    rsort_multi_last_stats (profiling on for the call)."""
     import threading
     sys.path.insert(0, str(PKG))
     import radixsort as rs
@@ -215,6 +216,9 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0):
     if capacity is None:
         capacity = sum(int(i[0].size) for i in inputs) + 1
     grp = rs.LoopbackGroup(world)
+    if stats is not None:
+        stats.extend([None] * world)
+        rs.multi_set_profiling(True)
     old_piece = rs.set_exchange_piece(piece) if piece else None
     old_opts = rs.set_multi_options(opts)
     dev_in = [(rs.from_numpy_u32(kx), rs.from_numpy_u32(vx) if vx is not None else None) for kx, vx in inputs]
@@ -226,10 +230,12 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0):
         try:
             with torch.cuda.stream(st):
                 kk, vv = dev_in[r]
-                ok, ov, off = rs.multi_sort_device(grp.transport(r), kk, k, vals=vv, capacity=capacity,
-                                                   stream=st)
+                tr = transports[r] if transports is not None else grp.transport(r)
+                ok, ov, off = rs.multi_sort_device(tr, kk, k, vals=vv, capacity=capacity, stream=st)
                 st.synchronize()
                 res[r] = (rs.to_numpy_u32(ok), rs.to_numpy_u32(ov) if ov is not None else None, off)
+                if stats is not None:
+                    stats[r] = rs.multi_last_stats()  # (thread-local: this rank's sort)
         except rs.RSortError as e:
             res[r] = e.status
 
@@ -240,6 +246,8 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0):
         t.join(timeout=240)
     alive = any(t.is_alive() for t in th)
     rs.set_multi_options(old_opts)
+    if stats is not None:
+        rs.multi_set_profiling(False)
     if old_piece:
         rs.set_exchange_piece(old_piece)
     if not alive:
@@ -325,6 +333,90 @@ def test_c_multi_loopback_local_error_on_every_rank():
     assert not any(t.is_alive() for t in th), "ranks left waiting"
     grp.close()
     assert res == [2] * world, res
+
+
+@pytest.mark.parametrize("stage,opts", [(1, 0), (1, 1), (2, 0), (2, 1)])
+def test_c_multi_loopback_failure_after_sample_gather(stage, opts):
+    """a rank that fails AFTER the sample all-gather (stage 1: its sample sort; stage 2:
+    its partition) still joins the count all-gather with a row of its peers' size and its status in
+    it, so every rank returns that status together (no mismatched collective, nobody left waiting)
+    -- with one and with two halves per rank (RSORT_MULTI_OVERLAP: 2 x world virtual ranks)."""
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    world = 3
+    inputs = [_loopback_inputs(r, 60_000, "uniform", False) for r in range(world)]
+    _check = rs._lib().rsort_multi_inject_failure
+    assert _check(1, stage, 6) == 0  # rank 1 fails with RSORT_ERR_HIP at this stage
+    try:
+        res = _run_loopback(world, inputs, 8, opts=opts)
+    finally:
+        _check(-1, 0, 0)
+    assert res == [6] * world, res
+    res = _run_loopback(world, inputs, 8, opts=opts)  # the hook cleared: the same sort succeeds
+    assert all(isinstance(x, tuple) for x in res), res
+    assert np.array_equal(np.concatenate([x[0] for x in res]), oracle_sort(np.concatenate([i[0] for i in inputs]), 8))
+
+
+@pytest.mark.parametrize("opts", [0, 1])
+def test_c_multi_loopback_stats(opts):
+    """rsort_multi_last_stats (bench.py's N-GPU block): per-thread records of each rank's sort --
+    world, halves, keys sent/received per peer (a rank's sends summed over ranks are what the ranks
+    receive), and the phase times, which add up to the total."""
+    world = 3
+    inputs = [_loopback_inputs(r, 200_000, "zipf", True) for r in range(world)]
+    st = []
+    res = _run_loopback(world, inputs, 8, opts=opts, stats=st)
+    assert all(isinstance(x, tuple) for x in res), res
+    for r, x in enumerate(st):
+        assert x["world"] == world and x["rank"] == r and x["halves"] == (2 if opts else 1) and x["direct"] == 0
+        assert x["bytes_per_key"] == 8 and x["n_in"] == inputs[r][0].size and x["n_out"] == res[r][0].size
+        assert sum(x["send_keys"]) == x["n_in"] and sum(x["recv_keys"]) == x["n_out"]
+        parts = x["ms_plan"] + x["ms_partition"] + x["ms_exchange"] + x["ms_local_sort"]
+        assert x["ms_total"] > 0 and abs(parts - x["ms_total"]) < 0.05 * x["ms_total"] + 0.05, x
+    for p in range(world):
+        assert sum(st[r]["send_keys"][p] for r in range(world)) == st[p]["n_out"]
+        assert [st[r]["send_keys"][p] for r in range(world)] == st[p]["recv_keys"]
+
+
+def test_c_multi_host_transport_threads():
+    """rsort_host_transport_wrap: the C protocol over a HOST-memory transport (the one bench.py's
+    gloo rehearsal uses), here three ranks as threads with a Python rendezvous; bit-exact as the
+    loopback, also with forced exchange rounds."""
+    import threading
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    world = 3
+    bar = threading.Barrier(world, timeout=120)
+    box = {}
+
+    def mk(r):
+        def allgather(send):
+            box[("ag", r)] = bytes(send)
+            bar.wait()
+            out = b"".join(box[("ag", q)] for q in range(world))
+            bar.wait()
+            return out
+
+        def exchange(sends, recv_sizes):
+            for p in range(world):
+                box[("ex", r, p)] = bytes(sends[p])
+            bar.wait()
+            out = [box[("ex", p, r)] for p in range(world)]
+            bar.wait()
+            return out
+        return rs.HostTransport(world, r, allgather, exchange)
+
+    hts = [mk(r) for r in range(world)]
+    inputs = [_loopback_inputs(r, 150_000, "hot", True) for r in range(world)]
+    try:
+        res = _run_loopback(world, inputs, 8, piece=20_000, transports=[h.transport for h in hts])
+    finally:
+        for h in hts:
+            h.close()
+    assert all(isinstance(x, tuple) for x in res), (res, [h.errors for h in hts])
+    rk, rv = oracle_sort_pairs(np.concatenate([i[0] for i in inputs]), np.concatenate([i[1] for i in inputs]), 8)
+    assert np.array_equal(np.concatenate([x[0] for x in res]), rk)
+    assert np.array_equal(np.concatenate([x[1] for x in res]), rv)
 
 
 @pytest.mark.parametrize("world,dist_name,pairs,k,piece", [(2, "uniform", False, 8, None), (3, "hot", True, 8, None),
