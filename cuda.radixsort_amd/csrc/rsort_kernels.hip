@@ -1317,7 +1317,13 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
 template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
-__global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
+#ifndef RSORT_LINES_MINW_SMALL
+#define RSORT_LINES_MINW_SMALL 1
+#endif
+#ifndef RSORT_NXR
+#define RSORT_NXR 8
+#endif
+__global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 1) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;
@@ -1350,7 +1356,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_lines(ScatterArgs a) {
     // share (digit, slot) -- a digit's lines are adjacent -- so without them ~4 lanes would hit
     // each of the R counters and serialise in the LDS
     constexpr bool NX = (R <= 16) && DMODE == kDigitShift;
-    constexpr uint32_t NXR = 8;
+    constexpr uint32_t NXR = RSORT_NXR;
     __shared__ uint32_t s_next[NX ? 2 * R * R * NXR : 1];
     __shared__ uint32_t s_nb[NX ? R : 1];  // first position of digit d's second output chunk
     __shared__ uint32_t s_oc[NX ? R : 1];  // digit d's first output chunk
