@@ -346,7 +346,7 @@ def is_partition_kernel(name):
     return name.split("<")[0] in ("rs_scatter", "rs_scatter_lines") and len(args) > 5 and args[5] == "1"
 
 
-def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt):
+def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt, steps):
     """The N-GPU block of the line: per-phase ms (mean over the profiled steps per rank, max over
     ranks), the exchange's bytes per rank and per peer link, and the local sort's and the partition's
     own scatter rooflines. per_rank: every rank's list of rsort_multi_stats dicts (one per step)."""
@@ -373,7 +373,7 @@ def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt):
         algo = 8 * t["keys"] / t["launches"] * (2 if last[0]["bytes_per_key"] == 8 else 1)
         return {"what": what, "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": int(algo),
                 "achieved": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "launches_per_step": t["launches"]}
+                "launches_per_step": t["launches"] // max(1, steps)}
 
     return {
         "transport": transport,
@@ -699,7 +699,7 @@ def main():
         }
         if use_dist and prof_c:
             line["multi"] = multi_summary(per_rank_stats, world, {"rccl_world": rccl_world}, transport, sc,
-                                          prof.times["partition"])
+                                          prof.times["partition"], a.steps)
         if configs:
             line["configs"] = configs
         if vendor:

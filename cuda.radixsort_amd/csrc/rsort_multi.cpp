@@ -419,6 +419,7 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         // keys go straight through the local sort (same output, no peers to agree with)
         if (local != RSORT_OK) return local;
         if (n > capacity) return RSORT_ERR_CAPACITY;
+        timer.mark(MultiTimer::kExchange);  // (nothing exchanged: the whole time is the local sort)
         if (n > 0) {
             rsort_plan p;
             if ((st = rsort_plan_make(n, k_bits, pairs, 0, &p))) return st;
@@ -430,7 +431,6 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         stats.halves = 1;
         stats.n_out = n;
         stats.send_keys[0] = stats.recv_keys[0] = n;
-        timer.mark(MultiTimer::kExchange);  // (nothing exchanged: the whole time is the local sort)
         return timer.finish(stats);
     }
     // RSORT_MULTI_OVERLAP: every rank's key range is cut in two (H = 2 virtual ranks per rank, the

@@ -144,3 +144,13 @@ def test_bench_one_rank_rccl_reports_phases():
                       "--no-cpu")
     assert d["verified"] is True and d["multi"]["rccl_world"] == 1
     check_multi_block(d, 1)
+
+
+def test_bench_one_rank_direct_phases():
+    """One rank without RSORT_MULTI_FULL sorts directly: the phase record is all local sort."""
+    d = run_bench_env({}, "--dist-path", "--steps", "2", "--warmup", "1", "--keys", str(1 << 22), "--no-cpu")
+    m = d["multi"]
+    assert d["verified"] is True and m["rccl_world"] == 1
+    ph = m["phases_ms_per_step"]
+    assert ph["local_sort"] >= 0.9 * ph["total"] and ph["exchange"] <= 0.1 * ph["total"], ph
+    assert m["local_sort_scatter"]["launches_per_step"] == d["config"]["passes"]
