@@ -774,8 +774,9 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 // C2 pass time) nor an acquire fence (~1.7 us) is needed. The table counts every key of the pass
 // exactly once, so its total must be `expect` (= n): the sum sweep checks that, and on a mismatch
 // (a late or stale line -- never observed) the workgroup takes the agent-scope acquire fence and
-// sums again; a second mismatch sets done[kDoneErr] (rsort_plan_check) -- so a visibility failure
-// is repaired or reported, never silent. All threads must call it.
+// sums again; a second mismatch sets done[kDoneErr] -- so a visibility failure is repaired, or
+// recorded where rsort_plan_check reads it (the sort itself still returns RSORT_OK: a caller that
+// must know asks rsort_plan_check after the sort, as rsort.h says). All threads must call it.
 template <int THREADS>
 __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t *done, uint32_t *s_ws,
                           uint32_t *s_flag, uint32_t expect) {
@@ -2556,12 +2557,15 @@ __global__ __launch_bounds__(THREADS) void rs_lane_order_probe(uint32_t *bad) {
         const uint32_t fn = (it / 8) % 4;
         const bool active = fn != 0 || (it % 3 == 0) || ((h >> 7) % 4 != 0);
         const uint32_t before = s_cnt[w * RS + d];
-        uint32_t below = 0;
-        for (int l = 0; l < kWave; ++l) {
-            const uint32_t dl = __shfl(d, l);  // every lane takes part (bpermute reads active lanes only)
-            const uint32_t al = __shfl(active ? 1u : 0u, l);
-            below += ((uint32_t)l < lane && al && dl == d) ? 1u : 0u;
+        // #lower active lanes with the same digit, from registers only: the lanes whose 8 digit bits
+        // all equal mine (8 ballots, every lane taking part), among the active ones
+        uint64_t same = __ballot(active);
+#pragma unroll
+        for (uint32_t b = 0; b < 8; ++b) {
+            const uint64_t ones = __ballot((d >> b) & 1u);
+            same &= ((d >> b) & 1u) ? ones : ~ones;
         }
+        const uint32_t below = (uint32_t)__popcll(same & lanes_below());
         __builtin_amdgcn_wave_barrier();
         if (active) {
             uint32_t got;
