@@ -96,6 +96,30 @@ def test_beyond_2_31_keys():
     assert torch.equal(out, ref)
 
 
+def test_near_2_32_keys_unaligned_output():
+    """n = 2^32 - 20 keys into an output 31 keys past a 128-B boundary. The whole-line
+    kernels count positions from the output's 128-B-aligned base, so n + 31 would not fit their 32-bit
+    positions: the passes into that output must take rs_scatter (and the sort fixed chunks) -- sorted, the input's
+    multiset, and the words around the output untouched. (~52 GB of device memory.)"""
+    n = (1 << 32) - 20
+    keys = rs.empty_u32(n)
+    rs.gen_uniform(keys, 0x2_32)
+    big = torch.full((n + 32 + 64,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    off = 32 + 31  # 128-B-aligned base + 31 keys (torch allocations are 256-B aligned)
+    out = big[off:off + n]
+    assert (out.data_ptr() & 127) == 124
+    rs.scatter_kernels_used(reset=True)
+    rs.sort_device(keys, out, 8)
+    used = rs.scatter_kernels_used(reset=True)
+    # the passes into `out` take rs_scatter; those into the (256-B-aligned) workspace keep the lines
+    assert any(k.startswith("rs_scatter<") for k in used), used
+    fp_in = rs.fingerprint(keys)[0]
+    del keys
+    assert rs.fingerprint(out) == (fp_in, 0)
+    torch.cuda.synchronize()
+    assert int((big[:off] != 0x5A5A5A5A).sum()) == 0 and int((big[off + n:] != 0x5A5A5A5A).sum()) == 0
+
+
 def test_fullsize_pairs_zipf():
     n = 1 << 30
     cdf = rs.from_numpy_u32(zipf_cdf_u32())
