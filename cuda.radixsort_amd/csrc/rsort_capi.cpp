@@ -9,6 +9,7 @@
 //   * errors are returned as rsort_status, never exit() (common.h:6-16).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -103,6 +104,17 @@ int device_cus() {
     return c;
 }
 
+// log2 of the smallest k = 4 keys-only sort on 1024-thread line tiles (default 28; RSORT_K4_LINES_LG in
+// the environment for A/B runs)
+int k4_lines_lg() {
+    static const int v = [] {
+        const char *e = getenv("RSORT_K4_LINES_LG");
+        const int x = e ? atoi(e) : 0;
+        return (x >= 16 && x <= 32) ? x : 28;
+    }();
+    return v;
+}
+
 // Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
 // 16384-key tiles (rs_scatter_lines), pairs from 8192-key tiles; k <= 4 keys
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
@@ -119,7 +131,7 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     if (k >= 5 && k <= 8 && !pairs && n >= enough * geom_tile_keys(kGeomLines)) return kGeomLines;
     // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:
     // 1.61 ms per pass against 1.75 ms with 4096-key tiles; at 2^26 0.120 against 0.113)
-    if (k == 4 && !pairs && n >= ((int64_t)1 << 28)) return kGeomLines;
+    if (k == 4 && !pairs && n >= ((int64_t)1 << k4_lines_lg())) return kGeomLines;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
     // lines: 2^26 keys, k = 4: 0.117 vs 0.144 ms per pass, dev/scatter_lab.hip); k <= 2 keeps
@@ -133,6 +145,16 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
 bool joint_plan(const rsort_plan &p) {
     return p.k_bits == kJointBits && p.num_chunks == (int64_t)kJointBins && p.passes >= 2 &&
            (geom_from_shape(p.threads, p.tile_keys, p.pairs) == (p.pairs ? kGeomLinesPairs : kGeomLines));
+}
+
+// RSORT_NX_TAIL=1 in the environment: next-digit plans scan each pass's table in its last workgroup
+// (the round-3 scheme) instead of every workgroup of the next pass summing the raw counts (A/B runs)
+bool nx_tail() {
+    static const bool v = [] {
+        const char *e = getenv("RSORT_NX_TAIL");
+        return e != nullptr && e[0] != '\0' && e[0] != '0';
+    }();
+    return v;
 }
 
 // Next-digit counts (rs_scatter_lines, k = 3, 4 keys): each pass adds the next pass's chunk table
@@ -188,7 +210,8 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     }
     if (!partition && next_plan(*p)) {
         ws += align256((size_t)p->table_entries * 4);  // the next pass's table
-        ws += 256;                                     // the tail-scan counter
+        ws += 256;                                     // the tail-scan counter / check words
+        ws += align256((size_t)p->table_entries * 4);  // raw-table offsets: the third table of the rotation
     }
     p->workspace_bytes = ws;
     return RSORT_OK;
@@ -205,7 +228,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done, *table3;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -237,6 +260,8 @@ Carve carve(const rsort_plan &p, void *ws) {
         c.table2 = (uint32_t *)q;
         q += align256((size_t)p.table_entries * 4);
         c.done = (uint32_t *)q;
+        q += 256;
+        c.table3 = (uint32_t *)q;
     }
     return c;
 }
@@ -336,8 +361,10 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
                const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr,
                uint32_t *next_table = nullptr, uint32_t *tail_zero = nullptr, uint32_t *done = nullptr,
-               const uint32_t *cl_select = nullptr) {
+               const uint32_t *cl_select = nullptr, int raw_table = 0, uint32_t *zero_table = nullptr) {
     ScatterArgs a{};
+    a.raw_table = raw_table ? 1u : 0u;
+    a.zero_table = zero_table;
     a.cl_select = cl_select;
     a.bounds = bounds;
     a.next_table = next_table;
@@ -359,8 +386,8 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
     const int geom = geom_from_shape(p.threads, p.tile_keys, p.pairs);
     if (!scatter_available(p.k_bits, p.pairs, rank, dmode, geom)) return RSORT_ERR_ARG;
     const int aligned16 = line_capable(kout, vout, p.pairs, p.n);
-    if ((bounds || next_table) && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
-        return RSORT_ERR_ARG;  // group chunks, next-digit counts: rs_scatter_lines only
+    if ((bounds || next_table || raw_table) && !(rank == kRankAtomic && aligned16 && !local_only && dmode == kDigitShift))
+        return RSORT_ERR_ARG;  // group chunks, next-digit counts, raw tables: rs_scatter_lines only
     // a multi-GPU partition's scatter (splitter digits) is recorded apart from the sort's passes
     PhaseScope ps(dmode == kDigitSplit ? RSORT_PHASE_PARTITION : RSORT_PHASE_SCATTER, p.n, s);
     return hip_status(launch_scatter(p.k_bits, p.pairs, rank, dmode, geom, local_only ? 0 : aligned16, a, s));
@@ -416,6 +443,11 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
                        line_capable(kout, nullptr, 0, p.n) && line_capable(c.tmp_k, nullptr, 0, p.n);
     if (next_plan(p) && !nextc && hipMemsetAsync(c.done, 0, 8, s) != hipSuccess)  // rsort_plan_check: clean
         return RSORT_ERR_HIP;
+    // next-digit plans: every pass after the first derives its offsets from the raw counts the pass
+    // before added (three tables in rotation: read / added into / cleared for the pass after next),
+    // instead of the last workgroup of each pass scanning them (RSORT_NX_TAIL=1: that older way)
+    const bool rawt = nextc && !nx_tail();
+    uint32_t *const rot[3] = {c.table, c.table2, c.table3};
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
         const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
@@ -424,9 +456,11 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // even pass i counts the joint counts for pass i + 1; odd pass i may use them
         const bool count_joint = joint && (i % 2 == 0) && i + 1 < P;
         const uint32_t *bounds = (joint && (i % 2 == 1)) ? c.bounds + (i / 2) * kBoundsWords : nullptr;
-        // next-digit plans alternate two tables: pass i reads tab, adds pass i + 1's into nxt
-        uint32_t *tab = (nextc && (i % 2 == 1)) ? c.table2 : c.table;
-        uint32_t *nxt = (nextc && i + 1 < P) ? ((i % 2 == 1) ? c.table : c.table2) : nullptr;
+        // next-digit plans alternate two tables (tail scans) or rotate three (raw tables): pass i
+        // reads tab, adds pass i + 1's into nxt
+        uint32_t *tab = rawt ? rot[i % 3] : (nextc && (i % 2 == 1)) ? c.table2 : c.table;
+        uint32_t *nxt = (nextc && i + 1 < P) ? (rawt ? rot[(i + 1) % 3] : (i % 2 == 1) ? c.table : c.table2) : nullptr;
+        uint32_t *clr = (rawt && i + 2 < P) ? rot[(i + 2) % 3] : nullptr;  // for the pass after next
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
@@ -447,7 +481,8 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // clustered-input kernel runs (rank_add_hot), else the plain one -- chosen on the device
         const uint32_t *cl = (joint && i >= 1) ? c.bounds + ((i - 1) / 2) * kBoundsWords : nullptr;
         if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt,
-                             nxt ? tab : nullptr, nxt ? c.done : nullptr, cl)))
+                             (nxt && !rawt) ? tab : nullptr, (nextc && (nxt || rawt)) ? c.done : nullptr, cl,
+                             rawt && i > 0, clr)))
             return st;
         sk = dk;
         sv = dv;

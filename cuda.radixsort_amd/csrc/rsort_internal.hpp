@@ -118,6 +118,13 @@ struct ScatterArgs {
     // aligned base and every output position up by pos_shift (< 32) keys, so lines are cache lines
     // for any 4-B-aligned output
     uint32_t pos_shift;
+    // rs_scatter_lines with k <= 4 (next-digit plans, passes after the first): raw_table = 1 -> `table`
+    // holds the previous pass's unscanned counts and every workgroup derives its own offsets from the
+    // whole table (no tail scan); done[kDoneErr] is set when the table's total is not n. zero_table:
+    // != nullptr -> each workgroup clears its R words of this R x num_chunks table (the one the pass
+    // after next counts into)
+    uint32_t raw_table;
+    uint32_t *zero_table;
 };
 
 struct ScanArgs {

@@ -1292,6 +1292,61 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     }
 }
 
+// ------------------------------------------------------------------------------ raw-table offsets
+// Next-digit plans (k = 3, 4), passes after the first: `table` holds the counts [d][c'] the previous
+// pass ADDED (unscanned). Every workgroup derives its own starts s_base[d] = (keys of every digit
+// below d) + (keys of digit d in chunks before c) from the whole table (R x C words: 64 KB at C2,
+// held in each XCD's L2 after the first reads) instead of one workgroup scanning it at the end of the
+// previous pass (tail_scan: ~5 us on the critical path of every pass). TPR = THREADS / R threads per
+// row, each summing every TPR-th quad of it. Returns false (in every thread) when the table does not
+// hold exactly n keys: the caller then writes nothing (no offset can leave the output), and workgroup
+// 0 records it for rsort_plan_check. All threads must call it; ends with a barrier.
+template <int THREADS, uint32_t R>
+__device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint64_t n, uint32_t *s_base,
+                            uint32_t *s_tot, uint32_t *err) {
+    constexpr uint32_t TPR = THREADS / R;
+    static_assert(TPR >= 1 && TPR <= (uint32_t)kWave && (TPR & (TPR - 1)) == 0, "a row's threads in one wave");
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t t = threadIdx.x, d = t / TPR, sub = t % TPR;
+    const uint32_t *row = table + (uint64_t)d * C;
+    uint32_t all = 0, below = 0;
+    if ((C & 3u) == 0u) {  // (rows start 16-B aligned: the table is)
+        const u32x4 *r4 = reinterpret_cast<const u32x4 *>(row);
+        for (uint32_t q = sub; q < C / 4u; q += TPR) {
+            const u32x4 v = r4[q];
+            const uint32_t c0 = q * 4u;
+            all += v.x + v.y + v.z + v.w;
+            below += (c0 < c ? v.x : 0u) + (c0 + 1u < c ? v.y : 0u) + (c0 + 2u < c ? v.z : 0u) + (c0 + 3u < c ? v.w : 0u);
+        }
+    } else {
+        for (uint32_t x = sub; x < C; x += TPR) {
+            const uint32_t v = row[x];
+            all += v;
+            below += x < c ? v : 0u;
+        }
+    }
+    uint32_t p0, tall, tbelow;
+    group_scan<TPR>(all, sub, p0, tall);
+    group_scan<TPR>(below, sub, p0, tbelow);
+    if (sub == 0) {
+        s_tot[d] = tall;
+        s_base[d] = tbelow;
+    }
+    __syncthreads();
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < R; ++i) tot += s_tot[i];  // (every thread: the same sum)
+    if (t < R) {
+        uint32_t pre = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < R; ++i) pre += i < t ? s_tot[i] : 0u;
+        s_base[t] += pre;
+        if (c == 0 && t == 0 && tot != n && err != nullptr) err[0] = 1u;
+    }
+    __syncthreads();
+    return tot == n;
+}
+
 // ------------------------------------------------------------------------------ small kernels
 // starts[d] = scanned table[d][0] (global start of digit d), starts[bins] = n.
 // ------------------------------------------------------------------------------ scatter (line-combining)
@@ -1362,6 +1417,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     __shared__ uint32_t s_nb[NX ? R : 1];  // first position of digit d's second output chunk
     __shared__ uint32_t s_oc[NX ? R : 1];  // digit d's first output chunk
     const bool count_next = NX && a.next_table != nullptr;
+    __shared__ uint32_t s_base[NX ? R : 1];  // raw-table offsets (ScatterArgs::raw_table)
+    __shared__ uint32_t s_rtot[NX ? R : 1];
 
     const uint32_t t = threadIdx.x;
     const uint32_t w = t / kWave;
@@ -1390,9 +1447,22 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     const bool leader = sub == 0;
     const uint32_t glead = lane & ~(TPD - 1u);
     uint32_t g_run = 0, carry = 0, inv = 0;
+    if constexpr (NX) {
+        // this workgroup's share of the table the pass after next counts into (nobody reads that
+        // one in this pass) is cleared on the way
+        if (a.zero_table != nullptr)
+            for (uint32_t i = t; i < R; i += THREADS) a.zero_table[(uint64_t)c * R + i] = 0u;
+        // this workgroup's starts from the previous pass's raw counts (a table that does not hold n
+        // keys -- never observed -- writes nothing: recorded for rsort_plan_check)
+        if (a.raw_table &&
+            !raw_offsets<THREADS, R>(a.table, a.num_chunks, c, a.n, s_base, s_rtot, a.done ? a.done + kDoneErr : nullptr))
+            return;
+    }
     if (leader) {
         // positions relative to kout's 128-B-aligned base (ScatterArgs::pos_shift): lines are cache lines
-        const uint32_t g0 = a.table[(uint64_t)d_own * a.num_chunks + c];
+        uint32_t g0;
+        if constexpr (NX) g0 = a.raw_table ? s_base[d_own] : a.table[(uint64_t)d_own * a.num_chunks + c];
+        else g0 = a.table[(uint64_t)d_own * a.num_chunks + c];
         const uint32_t g = g0 + a.pos_shift;
         carry = g & (G - 1u);  // the first line starts before the chunk's output
         inv = carry;
@@ -1740,8 +1810,9 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
                     atomicAdd(&a.next_table[(uint64_t)e * a.num_chunks + s_oc[d] + slot], v);
                 }
             }
-            // the last workgroup scans the next pass's table (no scan launches between passes)
-            if (a.done != nullptr) {
+            // the last workgroup scans the next pass's table (no scan launches between passes),
+            // unless the next pass derives its offsets from the raw counts itself (raw_table)
+            if (a.done != nullptr && a.tail_zero != nullptr) {
                 __shared__ uint32_t s_last;
                 tail_scan<THREADS>(a.next_table, (uint64_t)R * a.num_chunks, a.tail_zero, a.done, s_ws, &s_last,
                                    (uint32_t)a.n);

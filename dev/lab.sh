@@ -21,6 +21,8 @@
 #                    traces of the C3, Zipf-keys and all-equal benches
 #   ab V [CONFIGS]   the C3 line and the configs block (default zipf,c4): the built librsort.so and
 #                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels), alternating twice
+#   envab KV [CONFIGS] the C3 line and the configs block (default c2) with and without the library
+#                    environment setting KV (e.g. RSORT_NX_TAIL=1), alternating twice
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
@@ -158,6 +160,32 @@ PY
     done
     cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so
     rm -f gpurun_out/ab_new.so
+    ;;
+envab)
+    # the C3 line and a configs block (default c2) with and without an environment setting of the
+    # library, alternating twice: bash dev/lab.sh envab RSORT_NX_TAIL=1 [configs]
+    kv=$1
+    for side in new env new env; do
+        if [ "$side" = env ]; then
+            env "$kv" timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
+                --configs "${2:-c2}" > gpurun_out/envab_$side.json 2> gpurun_out/envab_$side.err
+        else
+            timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
+                --configs "${2:-c2}" > gpurun_out/envab_$side.json 2> gpurun_out/envab_$side.err
+        fi
+        stop_unless_ok $? "envab $side"
+        python3 - "$side" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/envab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+r = d["roofline"]
+print("%-6s C3    %8.3f ms/sort  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], d["ms_per_step"],
+      r["avg_launch_ms"], r["frac"], d["verified"]))
+for k, c in d["configs"].items():
+    print("%-6s %-5s %8.3f ms/sort  hist %.3f  scatter %.4f ms/pass (%.3f)  %s %s" % (sys.argv[1], k, c["ms_per_sort"],
+          c["phases_ms_per_sort"]["histogram"], c["scatter"]["avg_launch_ms"], c["scatter"]["frac"], c["verified"],
+          c["plan_check"]))
+PY
+    done
     ;;
 prof)
     tag=$1

@@ -154,3 +154,15 @@ def test_bench_one_rank_direct_phases():
     ph = m["phases_ms_per_step"]
     assert ph["local_sort"] >= 0.9 * ph["total"] and ph["exchange"] <= 0.1 * ph["total"], ph
     assert m["local_sort_scatter"]["launches_per_step"] == d["config"]["passes"]
+
+
+def test_bench_plain_gpus4_rehearsal_ragged():
+    """Four ranks on the one card (gloo host transport), an odd key count per rank and all-equal keys
+    (one equal-keys bucket split across every rank): the line, the checks and the per-rank record."""
+    d = run_bench_env({"RSORT_BENCH_BACKEND": "gloo"}, "--gpus", "4", "--steps", "1", "--warmup", "1",
+                      "--keys", str((1 << 20) + 77), "--dist", "equal", "--no-cpu")
+    assert d["n_gpus"] == 4 and d["verified"] is True
+    check_multi_block(d, 4)
+    # one key everywhere: the equal-keys bucket is cut across the ranks evenly
+    outs = d["multi"]["keys_out_per_rank"]
+    assert max(outs) - min(outs) <= 0.05 * sum(outs) / 4 + 64, outs
