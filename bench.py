@@ -324,6 +324,11 @@ def self_launch(a) -> int:
     re-execs; the children inherit stdout, so rank 0's JSON line is this command's output."""
     import socket
     import subprocess
+    visible = torch.cuda.device_count()  # (counts devices without initialising HIP on this image)
+    if os.environ.get("RSORT_BENCH_BACKEND", "") != "gloo" and visible < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but {visible} GPU(s) visible (RSORT_BENCH_BACKEND=gloo rehearses "
+              f"N ranks on fewer GPUs)", file=sys.stderr)
+        return 2
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
