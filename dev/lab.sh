@@ -23,6 +23,7 @@
 #                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels), alternating twice
 #   envab KV [CONFIGS] the C3 line and the configs block (default c2) with and without the library
 #                    environment setting KV (e.g. RSORT_NX_TAIL=1), alternating twice
+#   sqpmc            SQ counters (three passes) of a pairs pass (dev/pairs_lab) and a C3 sort (dev/sqpmc.py)
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
@@ -186,6 +187,26 @@ for k, c in d["configs"].items():
           c["plan_check"]))
 PY
     done
+    ;;
+sqpmc)
+    # SQ counters of one C4-shaped pairs pass (dev/pairs_lab, 2^29 pairs) and of a C3 sort (bench.py,
+    # 2^29 keys): three passes of <= 8 SQ counters each; dev/sqpmc.py summarises gpurun_out/sqpmc_*
+    P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM"
+    P2="SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"
+    P3="SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_BUSY_CYCLES"
+    i=0
+    for P in "$P1" "$P2" "$P3"; do
+        i=$((i + 1))
+        rm -rf "$R/gpurun_out/sqpmc_pairs_$i" "$R/gpurun_out/sqpmc_keys_$i"
+        (cd /tmp && PL_ROUNDS=1 PL_REPS=1 TMPDIR=/tmp timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv \
+            -d "$R/gpurun_out/sqpmc_pairs_$i" -- "$R/dev/pairs_lab" 29 > "$R/gpurun_out/sqpmc_pairs_$i.log" 2>&1)
+        stop_unless_ok $? "sqpmc pairs $i"
+        (cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$R/gpurun_out/sqpmc_keys_$i" -- \
+            python3 "$R/bench.py" --keys 536870912 --steps 1 --warmup 1 --no-cpu --no-e2e --no-vendor --configs "" \
+            > "$R/gpurun_out/sqpmc_keys_$i.log" 2>&1)
+        stop_unless_ok $? "sqpmc keys $i"
+    done
+    python3 dev/sqpmc.py gpurun_out
     ;;
 prof)
     tag=$1
