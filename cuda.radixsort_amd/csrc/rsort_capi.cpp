@@ -303,8 +303,12 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                  int dmode, const uint32_t *split, int nsplit, hipStream_t s,
                  const uint32_t *bounds = nullptr, uint32_t *copy_src = nullptr,
-                 const uint32_t *plan = nullptr, uint32_t *pcounts = nullptr) {
+                 const uint32_t *plan = nullptr, uint32_t *pcounts = nullptr, uint32_t *zero = nullptr,
+                 uint32_t *done = nullptr) {
     HistArgs a{};
+    a.zero = zero;
+    a.zero_n = zero ? (uint64_t)p.table_entries : 0u;
+    a.done = done;
     a.bounds = bounds;
     a.copy_src = copy_src;
     a.plan = plan;
@@ -468,12 +472,13 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
-                                      c.pcounts))) {
+                                      c.pcounts, rawt ? nxt : nullptr, rawt ? c.done : nullptr))) {
             return st;
         }
-        // next-digit plans: pass 0's table is scanned by launches (which also arm the tail
-        // counter); every later table was scanned by the previous scatter's last workgroup
-        if (!(nextc && i > 0) &&
+        // next-digit plans: pass 0's table is scanned by launches (which also arm the tail counter;
+        // raw tables: no scan at all, the histogram cleared the next table), every later table by the
+        // previous scatter's last workgroup (raw tables: by every workgroup of the pass itself)
+        if (!(nextc && i > 0) && !rawt &&
             (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds)))
             return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
@@ -482,7 +487,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         const uint32_t *cl = (joint && i >= 1) ? c.bounds + ((i - 1) / 2) * kBoundsWords : nullptr;
         if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt,
                              (nxt && !rawt) ? tab : nullptr, (nextc && (nxt || rawt)) ? c.done : nullptr, cl,
-                             rawt && i > 0, clr)))
+                             rawt, clr)))
             return st;
         sk = dk;
         sv = dv;

@@ -82,6 +82,12 @@ struct HistArgs {
     // (zeroed); joint_enable == nullptr or *joint_enable != kGroupsFixed turns the joint count on.
     uint32_t *joint;
     const uint32_t *joint_enable;
+    // raw-table next-digit plans (k = 3, 4), pass 0: the histogram also clears `zero` (zero_n words: the
+    // table pass 0's scatter counts into) and the check words done[0], done[kDoneErr]; its table is
+    // then read raw by the scatter (ScatterArgs::raw_table), with no scan launches
+    uint32_t *zero;
+    uint64_t zero_n;
+    uint32_t *done;
 };
 
 struct ScatterArgs {

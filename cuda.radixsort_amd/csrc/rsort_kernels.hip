@@ -529,6 +529,13 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
             return;
         }
     }
+    // raw-table plans (HistArgs::zero): clear the next table and the check words on the way
+    for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < a.zero_n; i += (uint64_t)gridDim.x * THREADS)
+        a.zero[i] = 0u;
+    if (a.done != nullptr && blockIdx.x == 0 && t == 0) {
+        a.done[0] = 0u;
+        a.done[kDoneErr] = 0u;
+    }
     for (uint32_t i = t; i < HW * R * SB; i += THREADS) s_h[i] = 0;
     __syncthreads();
 

@@ -187,9 +187,9 @@ RSORT_API int rsort_get_group_chunks(void);
 RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
                                 void *stream);
 /* After a sort with `plan` and `d_workspace` has completed on `stream`: *flags = 0 when every
- * on-device self-check of that sort passed; bit 0 = a k = 3, 4 tail scan found a next-pass table
- * whose total was not n even after an acquire fence and a second sweep (the sort's output is then
- * not trustworthy). Synchronises the stream. The sort entry points are stream-ordered and do not
+ * on-device self-check of that sort passed; bit 0 = a k = 3, 4 pass found the next-digit table it
+ * reads not holding n keys (the pass then wrote nothing; with RSORT_NX_TAIL=1: a tail scan found it
+ * so even after an acquire fence and a second sweep) -- the sort's output is then not trustworthy. Synchronises the stream. The sort entry points are stream-ordered and do not
  * wait for the device, so they CANNOT return this check: they return RSORT_OK for such a sort, and
  * this call is the only way to learn of it. rsort_u32_device / rsort_u32_pairs_device use the plan
  * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace; the host
