@@ -23,6 +23,7 @@
 #                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels), alternating twice
 #   envab KV [CONFIGS] the C3 line and the configs block (default c2) with and without the library
 #                    environment setting KV (e.g. RSORT_NX_TAIL=1), alternating twice
+#   sqzipf           SQ counters per pass of a Zipf-keys sort (LDS address / bank conflicts), in issue order
 #   sqpmc            SQ counters (three passes) of a pairs pass (dev/pairs_lab) and a C3 sort (dev/sqpmc.py)
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
@@ -207,6 +208,17 @@ sqpmc)
         stop_unless_ok $? "sqpmc keys $i"
     done
     python3 dev/sqpmc.py gpurun_out
+    ;;
+sqzipf)
+    # SQ counters per dispatch of the Zipf-keys passes (bench.py --dist zipf, 2^29 keys), in issue order:
+    # LDS address / bank conflicts of the clustered passes against the first (dev/sqpmc.py --order)
+    P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_ADDR_CONFLICT SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU"
+    rm -rf "$R/gpurun_out/sqzipf_keys_1"
+    (cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P1 --output-format csv -d "$R/gpurun_out/sqzipf_keys_1" -- \
+        python3 "$R/bench.py" --keys 536870912 --dist zipf --steps 1 --warmup 1 --no-cpu --no-e2e --no-vendor --configs "" \
+        > "$R/gpurun_out/sqzipf_keys_1.log" 2>&1)
+    stop_unless_ok $? "sqzipf"
+    python3 dev/sqpmc.py gpurun_out --order sqzipf_keys
     ;;
 prof)
     tag=$1

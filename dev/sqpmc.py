@@ -7,6 +7,22 @@ from collections import defaultdict
 from pathlib import Path
 
 root = Path(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
+if len(sys.argv) > 3 and sys.argv[2] == "--order":
+    # every working scatter dispatch of the run in issue order, one row each
+    rows = defaultdict(dict)
+    for f in (root / sys.argv[3] if (root / sys.argv[3]).is_dir() else root).rglob("*counter_collection.csv"):
+        if sys.argv[3] not in str(f):
+            continue
+        for r in csv.DictReader(open(f)):
+            if "rs_scatter" in r["Kernel_Name"]:
+                rows[(int(r["Dispatch_Id"]), r["Kernel_Name"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    names = None
+    for (did, kn), cs in sorted(rows.items()):
+        if cs.get("SQ_WAVE_CYCLES", 0) < 1e6:
+            continue
+        names = names or sorted(cs)
+        print(did, kn.split("(")[0].replace("void rsort::", "")[-12:], " ".join(f"{c[3:]}={cs[c]:.3g}" for c in names))
+    sys.exit(0)
 for prog in ("pairs", "keys"):
     agg = defaultdict(lambda: defaultdict(list))
     for d in sorted(root.glob(f"sqpmc_{prog}_*")):
