@@ -1379,13 +1379,34 @@ __device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint6
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
+// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup records its start and
+// end (s_memrealtime, 100 MHz) and its chunk [cbeg, cend) per pass (slot = shift / 8), read back with
+// rsort_lab_wg_times. Absent from the library.
+#ifdef RSORT_WG_TIMES
+__device__ unsigned long long g_wg_times[4][256][4];
+#define RS_WG_T0 const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();
+#define RS_WG_T1                                                                                  \
+    do {                                                                                          \
+        __syncthreads();                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x < 256) {                                               \
+            unsigned long long *p_ = g_wg_times[(a.shift / 8u) & 3u][blockIdx.x];                  \
+            p_[0] = wg_t0_;                                                                       \
+            p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
+            p_[2] = cbeg;                                                                         \
+            p_[3] = cend;                                                                         \
+        }                                                                                         \
+    } while (0)
+#else
+#define RS_WG_T0
+#define RS_WG_T1
+#endif
 #ifndef RSORT_LINES_MINW_SMALL
 #define RSORT_LINES_MINW_SMALL 1
 #endif
 #ifndef RSORT_NXR
 #define RSORT_NXR 8
 #endif
+template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
 __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 1) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
@@ -1438,6 +1459,7 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     // clustered-pass selection (ScatterArgs::cl_select): the plain and the clustered kernel are both
     // launched, and the one not selected by the device-side flag leaves at once
     if (a.cl_select != nullptr && ((*a.cl_select != kGroupsWhole) != (CL != 0))) return;
+    RS_WG_T0
     if (a.bounds != nullptr && a.bounds[0] != 0u) {
         // digit-group chunk (rs_histogram_joint): any start, so the tiles start at the 256-B
         // boundary below it (every wave load stays two whole 128-B lines), the first tile skips
@@ -1826,6 +1848,7 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
             }
         }
     }
+    RS_WG_T1;
 }
 
 // Lab builds (-DRSORT_STAMPS, dev/pairs_lab.hip): per-phase s_memtime cycle totals of thread 0 into
@@ -2869,3 +2892,9 @@ hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t
 }
 
 }  // namespace rsort
+
+#ifdef RSORT_WG_TIMES
+extern "C" __attribute__((visibility("default"))) int rsort_lab_wg_times(unsigned long long *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsort::g_wg_times), sizeof(rsort::g_wg_times)) == hipSuccess ? 0 : 6;
+}
+#endif

@@ -23,6 +23,7 @@
 #                    dev/var_V.so (dev/build_variant.sh; e.g. HEAD's kernels), alternating twice
 #   envab KV [CONFIGS] the C3 line and the configs block (default c2) with and without the library
 #                    environment setting KV (e.g. RSORT_NX_TAIL=1), alternating twice
+#   wgt [args]       per-workgroup durations of each scatter pass, slowest chunks of pass 1 (dev/wgtimes_lab.py)
 #   sqzipf           SQ counters per pass of a Zipf-keys sort (LDS address / bank conflicts), in issue order
 #   sqpmc            SQ counters (three passes) of a pairs pass (dev/pairs_lab) and a C3 sort (dev/sqpmc.py)
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
@@ -219,6 +220,21 @@ sqzipf)
         > "$R/gpurun_out/sqzipf_keys_1.log" 2>&1)
     stop_unless_ok $? "sqzipf"
     python3 dev/sqpmc.py gpurun_out --order sqzipf_keys
+    ;;
+wgt)
+    # per-workgroup durations of every scatter pass (dev/var_wgt.so: -DRSORT_WG_TIMES) and what the
+    # slowest chunks of pass 1 hold: Zipf keys, Zipf pairs, uniform keys (dev/wgtimes_lab.py)
+    cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
+    cp dev/var_wgt.so cuda.radixsort_amd/librsort.so
+    for args in "--dist zipf" "--dist zipf --pairs" "--dist uniform"; do
+        timeout -k 10 240 python dev/wgtimes_lab.py $args "$@" >> gpurun_out/wgt.log 2>&1
+        rc=$?
+        echo "[lab] wgt $args rc=$rc"
+        [ $rc -eq 0 ] || break
+    done
+    cp gpurun_out/wgt_lib.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/wgt_lib.so
+    cat gpurun_out/wgt.log
     ;;
 prof)
     tag=$1

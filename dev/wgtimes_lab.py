@@ -1,0 +1,77 @@
+"""Per-workgroup durations of a sort's scatter passes (dev/var_wgt.so: the library built with
+-DRSORT_WG_TIMES, copied over cuda.radixsort_amd/librsort.so on the box first) and, for the pass
+given, what the slowest and fastest chunks hold. Backs DESIGN §8 round 4 item 4 (Zipf pass 1).
+
+    python dev/wgtimes_lab.py [--dist zipf] [--log2n 29] [--pass 1] [--pairs]
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "cuda.radixsort_amd"))
+sys.path.insert(0, str(ROOT / "tests"))
+import radixsort as rs  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--dist", default="zipf")
+ap.add_argument("--log2n", type=int, default=29)
+ap.add_argument("--pass", dest="pss", type=int, default=1)
+ap.add_argument("--pairs", action="store_true")
+a = ap.parse_args()
+n = 1 << a.log2n
+lib = rs._lib()
+fn = lib.rsort_lab_wg_times
+fn.argtypes = [ctypes.c_void_p]
+fn.restype = ctypes.c_int
+keys = rs.empty_u32(n)
+if a.dist == "zipf":
+    from _util import zipf_cdf_u32
+    rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32()), 0x5EED)
+else:
+    rs.gen_uniform(keys, 0x5EED)
+vals = None
+if a.pairs:
+    vals = rs.empty_u32(n)
+    rs.gen_iota(vals, 0)
+out = rs.empty_u32(n)
+vout = rs.empty_u32(n) if a.pairs else None
+p = rs.plan(n, 8, a.pairs)
+ws = rs.workspace(p.workspace_bytes)
+for _ in range(3):
+    rs.sort_device(keys, out, 8, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
+torch.cuda.synchronize()
+buf = np.zeros((4, 256, 4), dtype=np.uint64)
+assert fn(buf.ctypes.data) == 0
+print("modes", rs.group_flags(p, ws))
+for ps in range(4):
+    t0, t1, cb, ce = (buf[ps, :, i].astype(np.int64) for i in range(4))
+    dur = (t1 - t0) * 10 / 1e3  # 100 MHz ticks -> us
+    start = (t0 - t0.min()) * 10 / 1e3
+    size = ce - cb
+    print(f"pass {ps}: wall {((t1.max() - t0.min()) * 10 / 1e3):8.1f} us  per-wg dur min/med/max "
+          f"{dur.min():7.1f} {np.median(dur):7.1f} {dur.max():7.1f}  start spread {start.max():5.1f} us  "
+          f"keys/chunk min/max {size.min()} {size.max()}  us per Mkey min/med/max "
+          f"{(dur / size * 1e6).min():.1f} {np.median(dur / size * 1e6):.1f} {(dur / size * 1e6).max():.1f}")
+# the chunks of the pass asked for: what they hold (its input = the previous pass's output: the keys
+# stably sorted by the lower digits, computed here)
+ps = a.pss
+h = rs.to_numpy_u32(keys)
+inp = h[np.argsort(h & ((1 << (8 * ps)) - 1), kind="stable")] if ps > 0 else h
+t0, t1, cb, ce = (buf[ps, :, i].astype(np.int64) for i in range(4))
+dur = (t1 - t0) * 10 / 1e3
+order = np.argsort(dur)
+print(f"\npass {ps} chunks, slowest and fastest: us, keys, top key share, distinct digits, top digit share, "
+      f"distinct keys, distinct lower-digit groups")
+for c in list(order[-12:][::-1]) + list(order[:6]):
+    x = inp[cb[c]:ce[c]]
+    d = (x >> (8 * ps)) & 255
+    u, cnt = np.unique(x, return_counts=True)
+    du, dcnt = np.unique(d, return_counts=True)
+    g = np.unique(x & ((1 << (8 * ps)) - 1)).size if ps > 0 else 0
+    print(f"  chunk {c:3d} {dur[c]:8.1f} us {x.size:9d}  top key {cnt.max() / x.size:.3f}  digits {du.size:3d}  "
+          f"top digit {dcnt.max() / x.size:.3f}  keys {u.size:8d}  groups {g}")
