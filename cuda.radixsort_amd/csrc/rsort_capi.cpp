@@ -147,6 +147,15 @@ bool joint_plan(const rsort_plan &p) {
            (geom_from_shape(p.threads, p.tile_keys, p.pairs) == (p.pairs ? kGeomLinesPairs : kGeomLines));
 }
 
+// RSORT_CUT_WEIGHTS=0 in the environment: cut plans with equal key counts per chunk (A/B runs)
+bool cut_weights() {
+    static const bool v = [] {
+        const char *e = getenv("RSORT_CUT_WEIGHTS");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return v;
+}
+
 // RSORT_NX_TAIL=1 in the environment: next-digit plans scan each pass's table in its last workgroup
 // (the round-3 scheme) instead of every workgroup of the next pass summing the raw counts (A/B runs)
 bool nx_tail() {
@@ -296,8 +305,11 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
     // group boundary up to half a tile (and a quarter chunk) away
     const uint32_t snap = (uint32_t)std::min<int64_t>(p.tile_keys / 2, p.n / (4 * (int64_t)kJointBins));
+    // the first cut plan of a sort (pass 1's, from pass 0's joint counts) balances estimated cost
+    // (rs_joint_bounds; RSORT_CUT_WEIGHTS=0 turns it off for A/B runs)
+    const uint32_t weighted = (enable == nullptr && cut_weights()) ? 1u : 0u;
     return hip_status(launch_joint_bounds(joint, enable, bounds, plan, pcounts, (uint64_t)p.n,
-                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, s));
+                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, weighted, s));
 }
 
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,

@@ -181,10 +181,11 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
 // From the joint counts [next digit][group]: the next pass's chunks into bounds[1..R+1] and its
 // mode into bounds[0] (above): kGroupsWhole when every group fits in max_keys keys, else the cut
 // plan (plan, pcounts rows zeroed); kGroupsFixed when the counts do not add up to n or enable
-// says the joint count was off (HistArgs::joint_enable).
+// says the joint count was off (HistArgs::joint_enable). weighted != 0: a cut plan's chunks get
+// equal estimated cost instead of equal key counts (rs_joint_bounds).
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
-                               uint32_t snap, hipStream_t s);
+                               uint32_t snap, uint32_t weighted, hipStream_t s);
 // rank_algo: internal RankAlgo. aligned16: the whole-line kernels may run -- keys-only: always
 // (any 4-B-aligned kout; launch_scatter shifts positions to kout's 128-B-aligned base); pairs: when
 // (vout - kout) % 16 == 0 (otherwise the same plan runs rs_scatter with the same tiles).

@@ -873,12 +873,25 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
 // exclusive scan = the groups' first key positions in the previous pass's output, and the next
 // pass's chunk mode (kGroupsWhole / kGroupsCut / kGroupsFixed, rsort_internal.hpp) with its
 // chunk starts; for kGroupsCut also the cut plan and zeroed piece rows.
+// Cost-weighted cut plans (weighted != 0): the chunks of the next pass get equal estimated COST, not
+// equal key counts. A group's keys arrive at the clustered scatter kernel in input order, so a
+// chunk's per-key cost follows the group's next-digit distribution p (its joint column / size):
+// measured on 2^28 Zipf keys, pass 1 (dev/wgtimes_lab.py, per-workgroup times of all 256 chunks, refit
+// on the weighted plan's own chunks), us per Mkey = 427.1 + 685.9 * (sum p^2 - top^2) + 17.6 * top -
+// 37.2 * top^2 (top = the largest p; the ranking aggregates the top digit, the other shared digits
+// serialise), residual sd ~10 against a 400-518 spread with equal key counts. Weights are that rate
+// over its constant, clamped to [0.8, 1.4].
 __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, const uint32_t *enable,
                                                         uint32_t *bounds, uint32_t *plan, uint32_t *pcounts,
-                                                        uint64_t n, uint64_t max_keys, uint32_t snap) {
+                                                        uint64_t n, uint64_t max_keys, uint32_t snap,
+                                                        uint32_t weighted) {
     constexpr uint32_t R = kJointBins;
     constexpr uint32_t Q = 1024 / R;
     __shared__ uint32_t s_part[Q][R];
+    __shared__ float s_sq[Q][R];                   // per part: sum of squared joint counts
+    __shared__ uint32_t s_mx[Q][R];                // per part: the largest joint count
+    __shared__ float s_w[R];                       // per group: cost per key (weighted plans)
+    __shared__ uint32_t s_C[R + 1];                // per group: first weighted key (weighted plans)
     __shared__ uint32_t s_ws[1024 / kWave];
     __shared__ uint32_t s_max;
     __shared__ uint32_t s_b[R + 1];                // group starts
@@ -892,9 +905,17 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
         return;
     }
     const uint32_t g = t % R, q = t / R;
-    uint32_t s = 0;
-    for (uint32_t e = q * (R / Q); e < (q + 1) * (R / Q); ++e) s += joint[e * R + g];
+    uint32_t s = 0, mx = 0;
+    float sq = 0.f;
+    for (uint32_t e = q * (R / Q); e < (q + 1) * (R / Q); ++e) {
+        const uint32_t v = joint[e * R + g];
+        s += v;
+        mx = max(mx, v);
+        sq += (float)v * (float)v;
+    }
     s_part[q][g] = s;
+    s_sq[q][g] = sq;
+    s_mx[q][g] = mx;
     if (t == 0) s_max = 0u;
     __syncthreads();
     uint32_t tot = 0;
@@ -940,8 +961,49 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
         }
         return lo;
     };
+    // weighted plans: per group the cost per key from its next-digit distribution, and the groups'
+    // first weighted keys (units of 4 weighted keys: the total stays below 2^32)
+    uint32_t WK = 0;
+    if (weighted) {
+        uint32_t wk = 0;
+        if (t < R) {
+            float w = 1.f;
+            if (tot > 0) {
+                float sqs = 0.f;
+                uint32_t m = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < Q; ++i) {
+                    sqs += s_sq[i][t];
+                    m = max(m, s_mx[i][t]);
+                }
+                const float inv = 1.f / (float)tot, top = (float)m * inv, h = sqs * inv * inv;
+                w = (427.1f + 685.9f * fmaxf(h - top * top, 0.f) + 17.6f * top - 37.2f * top * top) / 427.1f;
+                w = fminf(fmaxf(w, 0.8f), 1.4f);
+            }
+            s_w[t] = w;
+            wk = (uint32_t)((float)tot * w * 0.25f);
+        }
+        const uint32_t c0 = block_excl_scan<1024>(wk, s_ws, WK);
+        if (t < R) s_C[t] = c0;
+        if (t == 0) s_C[R] = WK;
+        __syncthreads();
+    }
     if (t <= R) {
         uint32_t B = (uint32_t)((n * t) / R);
+        if (weighted && t > 0 && t < R) {
+            // the position where the weighted keys reach t / R of their total: the last group starting
+            // at or below that weight, and inside it by its cost per key
+            const uint32_t target = (uint32_t)(((uint64_t)WK * t) / R);
+            uint32_t lo = 0, hi = R - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (s_C[mid] <= target) lo = mid;
+                else hi = mid - 1;
+            }
+            const float off = (float)(target - s_C[lo]) * 4.f / s_w[lo];
+            const uint32_t len = s_b[lo + 1] - s_b[lo];
+            B = s_b[lo] + min((uint32_t)off, len);
+        }
         if (t > 0 && t < R) {
             // snap to the nearer group boundary when it is within `snap` keys
             const uint32_t gg = group_of(B);
@@ -2815,8 +2877,8 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
 
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
-                               uint32_t snap, hipStream_t s) {
-    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap);
+                               uint32_t snap, uint32_t weighted, hipStream_t s) {
+    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap, weighted);
     return hipGetLastError();
 }
 

@@ -226,7 +226,8 @@ wgt)
     # slowest chunks of pass 1 hold: Zipf keys, Zipf pairs, uniform keys (dev/wgtimes_lab.py)
     cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
     cp dev/var_wgt.so cuda.radixsort_amd/librsort.so
-    for args in "--dist zipf" "--dist zipf --pairs" "--dist uniform"; do
+    for args in "--dist zipf --dump gpurun_out/wgt_zipf_p1.csv" "--dist zipf --pass 2 --dump gpurun_out/wgt_zipf_p2.csv" \
+                "--dist uniform"; do
         timeout -k 10 240 python dev/wgtimes_lab.py $args "$@" >> gpurun_out/wgt.log 2>&1
         rc=$?
         echo "[lab] wgt $args rc=$rc"

@@ -674,7 +674,7 @@ int main(int argc, char **argv) {
         hj.keys = c.keys; hj.table = c.table; hj.n = c.n; hj.chunk_keys = c.n / 256; hj.num_chunks = 256;
         hj.shift = 0; hj.vec = 1; hj.split = 1; hj.joint = c.joint;
         CK(launch_histogram_joint(hj, 0));
-        CK(launch_joint_bounds(c.joint, nullptr, c.bounds, nullptr, nullptr, c.n, c.n / 256 + 16384, 0, 0));
+        CK(launch_joint_bounds(c.joint, nullptr, c.bounds, nullptr, nullptr, c.n, c.n / 256 + 16384, 0, 0, 0));
         c.groups = true;
     }
     for (int i = 0; i < npre; ++i) {

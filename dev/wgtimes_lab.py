@@ -22,6 +22,7 @@ ap.add_argument("--dist", default="zipf")
 ap.add_argument("--log2n", type=int, default=29)
 ap.add_argument("--pass", dest="pss", type=int, default=1)
 ap.add_argument("--pairs", action="store_true")
+ap.add_argument("--dump", default="", help="write every chunk of the pass as CSV (us, keys, top digit share, H)")
 a = ap.parse_args()
 n = 1 << a.log2n
 lib = rs._lib()
@@ -75,3 +76,16 @@ for c in list(order[-12:][::-1]) + list(order[:6]):
     g = np.unique(x & ((1 << (8 * ps)) - 1)).size if ps > 0 else 0
     print(f"  chunk {c:3d} {dur[c]:8.1f} us {x.size:9d}  top key {cnt.max() / x.size:.3f}  digits {du.size:3d}  "
           f"top digit {dcnt.max() / x.size:.3f}  keys {u.size:8d}  groups {g}")
+
+if a.dump:
+    with open(a.dump, "w") as fh:
+        fh.write("chunk,us,keys,top_digit,herfindahl,digits,groups\n")
+        for c in range(256):
+            x = inp[cb[c]:ce[c]]
+            if x.size == 0:
+                continue
+            d = (x >> (8 * ps)) & 255
+            dc = np.bincount(d, minlength=256) / x.size
+            g = np.unique(x & ((1 << (8 * ps)) - 1)).size if ps > 0 else 0
+            fh.write(f"{c},{dur[c]:.1f},{x.size},{dc.max():.4f},{(dc * dc).sum():.5f},{(dc > 0).sum()},{g}\n")
+    print("wrote", a.dump)
