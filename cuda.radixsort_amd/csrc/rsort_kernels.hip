@@ -377,6 +377,31 @@ struct Digit {
     }
 };
 
+// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup (and every joint-count
+// histogram workgroup, g_wg_htimes) records its start and end (s_memrealtime, 100 MHz) and its key range
+// [beg, end) per pass (slot = shift / 8), read back with rsort_lab_wg_times. Absent from the library.
+#ifdef RSORT_WG_TIMES
+__device__ unsigned long long g_wg_times[4][256][4];
+__device__ unsigned long long g_wg_htimes[4][256][4];
+#define RS_WG_T0 const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();
+#define RS_WG_TREC(TAB, B, E)                                                                     \
+    do {                                                                                          \
+        __syncthreads();                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x < 256) {                                               \
+            unsigned long long *p_ = TAB[(a.shift / 8u) & 3u][blockIdx.x];                         \
+            p_[0] = wg_t0_;                                                                       \
+            p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
+            p_[2] = (B);                                                                          \
+            p_[3] = (E);                                                                          \
+        }                                                                                         \
+    } while (0)
+#define RS_WG_T1 RS_WG_TREC(g_wg_times, cbeg, cend)
+#define RS_WG_TH1 RS_WG_TREC(g_wg_htimes, beg, end)
+#else
+#define RS_WG_T0
+#define RS_WG_T1
+#define RS_WG_TH1
+#endif
 // ------------------------------------------------------------------------------ histogram
 // Reference: histogramKernel (Parallel7.cu:318-343) + transpose (P7:361-392, :596).
 // SUB: each per-wave copy is split into SUB interleaved sub-counters (lane % SUB picks one), so
@@ -400,6 +425,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t *s_sp = s_j + R * RS;
     const uint32_t t = threadIdx.x;
+    RS_WG_T0
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
@@ -497,6 +523,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         const uint32_t v = (s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu;
         if (v) atomicAdd(&a.joint[item], v);
     }
+    RS_WG_TH1;
 }
 
 template <int BITS, int THREADS, int DMODE, int NT = 0, int SUB = 1, bool JOINT = false>
@@ -1441,27 +1468,6 @@ __device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint6
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup records its start and
-// end (s_memrealtime, 100 MHz) and its chunk [cbeg, cend) per pass (slot = shift / 8), read back with
-// rsort_lab_wg_times. Absent from the library.
-#ifdef RSORT_WG_TIMES
-__device__ unsigned long long g_wg_times[4][256][4];
-#define RS_WG_T0 const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();
-#define RS_WG_T1                                                                                  \
-    do {                                                                                          \
-        __syncthreads();                                                                          \
-        if (threadIdx.x == 0 && blockIdx.x < 256) {                                               \
-            unsigned long long *p_ = g_wg_times[(a.shift / 8u) & 3u][blockIdx.x];                  \
-            p_[0] = wg_t0_;                                                                       \
-            p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
-            p_[2] = cbeg;                                                                         \
-            p_[3] = cend;                                                                         \
-        }                                                                                         \
-    } while (0)
-#else
-#define RS_WG_T0
-#define RS_WG_T1
-#endif
 #ifndef RSORT_LINES_MINW_SMALL
 #define RSORT_LINES_MINW_SMALL 1
 #endif
@@ -2957,6 +2963,10 @@ hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t
 
 #ifdef RSORT_WG_TIMES
 extern "C" __attribute__((visibility("default"))) int rsort_lab_wg_times(unsigned long long *host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsort::g_wg_times), sizeof(rsort::g_wg_times)) == hipSuccess ? 0 : 6;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsort::g_wg_times), sizeof(rsort::g_wg_times)) == hipSuccess &&
+                   hipMemcpyFromSymbol(host + 4 * 256 * 4, HIP_SYMBOL(rsort::g_wg_htimes), sizeof(rsort::g_wg_htimes)) ==
+                       hipSuccess
+               ? 0
+               : 6;
 }
 #endif

@@ -237,6 +237,22 @@ wgt)
     rm -f gpurun_out/wgt_lib.so
     cat gpurun_out/wgt.log
     ;;
+wgth)
+    # the same lab build: per-workgroup durations of the joint-count histograms (Zipf, uniform keys;
+    # WGT_VAR picks another lab build dev/var_$WGT_VAR.so, WGT_DISTS the distributions)
+    cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
+    cp dev/var_${WGT_VAR:-wgt}.so cuda.radixsort_amd/librsort.so
+    echo "== ${WGT_VAR:-wgt}" >> gpurun_out/wgth.log
+    for dist in ${WGT_DISTS:-zipf uniform}; do
+        timeout -k 10 240 python dev/wgtimes_lab.py --dist $dist --hist "$@" >> gpurun_out/wgth.log 2>&1
+        rc=$?
+        echo "[lab] wgth $dist rc=$rc"
+        [ $rc -eq 0 ] || break
+    done
+    cp gpurun_out/wgt_lib.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/wgt_lib.so
+    cat gpurun_out/wgth.log
+    ;;
 prof)
     tag=$1
     shift

@@ -23,6 +23,8 @@ ap.add_argument("--log2n", type=int, default=29)
 ap.add_argument("--pass", dest="pss", type=int, default=1)
 ap.add_argument("--pairs", action="store_true")
 ap.add_argument("--dump", default="", help="write every chunk of the pass as CSV (us, keys, top digit share, H)")
+ap.add_argument("--hist", action="store_true",
+                help="also the joint-count histograms (passes 0 and 2) and what the slowest pass-2 chunks hold")
 a = ap.parse_args()
 n = 1 << a.log2n
 lib = rs._lib()
@@ -46,8 +48,9 @@ ws = rs.workspace(p.workspace_bytes)
 for _ in range(3):
     rs.sort_device(keys, out, 8, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
 torch.cuda.synchronize()
-buf = np.zeros((4, 256, 4), dtype=np.uint64)
-assert fn(buf.ctypes.data) == 0
+both = np.zeros((2, 4, 256, 4), dtype=np.uint64)
+assert fn(both.ctypes.data) == 0
+buf, hbuf = both[0], both[1]
 print("modes", rs.group_flags(p, ws))
 for ps in range(4):
     t0, t1, cb, ce = (buf[ps, :, i].astype(np.int64) for i in range(4))
@@ -89,3 +92,26 @@ if a.dump:
             g = np.unique(x & ((1 << (8 * ps)) - 1)).size if ps > 0 else 0
             fh.write(f"{c},{dur[c]:.1f},{x.size},{dc.max():.4f},{(dc * dc).sum():.5f},{(dc > 0).sum()},{g}\n")
     print("wrote", a.dump)
+
+if a.hist:
+    print()
+    for ps in (0, 2):
+        t0, t1, cb, ce = (hbuf[ps, :, i].astype(np.int64) for i in range(4))
+        dur = (t1 - t0) * 10 / 1e3
+        print(f"joint histogram pass {ps}: wall {((t1.max() - t0.min()) * 10 / 1e3):8.1f} us  per-wg dur min/med/max "
+              f"{dur.min():7.1f} {np.median(dur):7.1f} {dur.max():7.1f}  keys/chunk {(ce - cb).max()}")
+    # pass 2's histogram input: the keys sorted by their low 16 bits; it counts (digit 2, digit 3)
+    t0, t1, cb, ce = (hbuf[2, :, i].astype(np.int64) for i in range(4))
+    dur = (t1 - t0) * 10 / 1e3
+    inp = h[np.argsort(h & 0xFFFF, kind="stable")]
+    print("pass 2 joint-count chunks, slowest and fastest: us, top pair share, distinct pairs, mean pair run, "
+          "keys in runs >= 4, quads with one pair")
+    for c in list(np.argsort(dur)[-10:][::-1]) + list(np.argsort(dur)[:6]):
+        x = inp[cb[c]:ce[c]] >> 16
+        u, cnt = np.unique(x, return_counts=True)
+        brk = np.flatnonzero(np.diff(x) != 0)
+        runs = np.diff(np.concatenate(([0], brk + 1, [x.size])))
+        q = x[: x.size // 4 * 4].reshape(-1, 4)
+        one = (q == q[:, :1]).all(axis=1).mean()
+        print(f"  chunk {c:3d} {dur[c]:8.1f} us  top pair {cnt.max() / x.size:.3f}  pairs {u.size:8d}  run "
+              f"{x.size / runs.size:7.2f}  in runs>=4 {runs[runs >= 4].sum() / x.size:.3f}  one-pair quads {one:.3f}")
