@@ -580,7 +580,12 @@ int host_sort(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t
         return RSORT_ERR_HIP;
     if (pairs && hipMemcpyAsync(vout, d_vout, (size_t)n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return RSORT_ERR_HIP;
-    return hip_status(hipStreamSynchronize(s));
+    // this entry waits for the device anyway: the sort's self-check (rsort_plan_check) is read here
+    uint32_t check = 0;
+    if (next_plan(p) && hipMemcpyAsync(&check, carve(p, ws).done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    return check ? RSORT_ERR_CHECK : RSORT_OK;
 }
 
 }  // namespace
@@ -603,6 +608,7 @@ const char *rsort_status_string(int status) {
         case RSORT_ERR_NODEV: return "no HIP device";
         case RSORT_ERR_CAPACITY: return "output capacity too small for the received keys";
         case RSORT_ERR_COMM: return "RCCL communication error";
+        case RSORT_ERR_CHECK: return "an on-device self-check of the sort failed";
         default: return "unknown status";
     }
 }

@@ -39,7 +39,7 @@ RSORT_OK = 0
 STATUS_NAMES = {0: "RSORT_OK", 1: "RSORT_ERR_ARG", 2: "RSORT_ERR_BITS", 3: "RSORT_ERR_SIZE",
                 4: "RSORT_ERR_ALIGN", 5: "RSORT_ERR_ALLOC", 6: "RSORT_ERR_HIP",
                 7: "RSORT_ERR_WORKSPACE", 8: "RSORT_ERR_NODEV", 9: "RSORT_ERR_CAPACITY",
-                10: "RSORT_ERR_COMM"}
+                10: "RSORT_ERR_COMM", 11: "RSORT_ERR_CHECK"}
 RANK_MATCH, RANK_SPLIT, RANK_BALLOT = 0, 1, 2
 PHASES = ("histogram", "scan", "scatter", "copy", "partition")
 

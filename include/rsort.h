@@ -60,7 +60,8 @@ typedef enum rsort_status {
     RSORT_ERR_WORKSPACE = 7,  /* workspace too small */
     RSORT_ERR_NODEV = 8,      /* no HIP device visible */
     RSORT_ERR_CAPACITY = 9,   /* multi-GPU: this rank receives more keys than its output holds */
-    RSORT_ERR_COMM = 10       /* multi-GPU: an RCCL call failed */
+    RSORT_ERR_COMM = 10,      /* multi-GPU: an RCCL call failed */
+    RSORT_ERR_CHECK = 11      /* host entries: an on-device self-check of the sort failed (rsort_plan_check) */
 } rsort_status;
 
 /* Local-rank algorithm inside a tile (all give the same, unique, stable result). */
@@ -192,9 +193,9 @@ RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace,
  * so even after an acquire fence and a second sweep) -- the sort's output is then not trustworthy. Synchronises the stream. The sort entry points are stream-ordered and do not
  * wait for the device, so they CANNOT return this check: they return RSORT_OK for such a sort, and
  * this call is the only way to learn of it. rsort_u32_device / rsort_u32_pairs_device use the plan
- * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace; the host
- * entries (rsort_u32, rsort_u32_ex, rsort_u32_pairs) use a library-owned workspace and cannot be
- * queried -- use the device entries where the check matters. Never observed failing. */
+ * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace. The host
+ * entries (rsort_u32, rsort_u32_ex, rsort_u32_pairs) wait for the device anyway: they read the check
+ * themselves and return RSORT_ERR_CHECK for such a sort. Never observed failing. */
 RSORT_API int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream);
 /* The scatter kernel instantiations this library has launched since the last reset, ';'-joined
  * into buf (at most len - 1 characters and a NUL); returns the full length. reset != 0 clears the

@@ -35,8 +35,10 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_status_strings():
     lib = rs._lib()
-    for st in range(9):
-        assert lib.rsort_status_string(st)
+    for st in range(12):
+        assert lib.rsort_status_string(st) != b"unknown status", st
+        assert rs.STATUS_NAMES[st].startswith("RSORT_")
+    assert lib.rsort_status_string(12) == b"unknown status"
     assert lib.rsort_status_string(2) == b"k_bits outside [1, 13]"
 
 
