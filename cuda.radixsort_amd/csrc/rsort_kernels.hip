@@ -377,26 +377,27 @@ struct Digit {
     }
 };
 
-// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup (and every joint-count
-// histogram workgroup, g_wg_htimes) records its start and end (s_memrealtime, 100 MHz) and its key range
-// [beg, end) per pass (slot = shift / 8), read back with rsort_lab_wg_times. Absent from the library.
+// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup (the first 2048 of a
+// pass; slot = shift / BITS) and every joint-count histogram workgroup (g_wg_htimes, slot = shift / 8)
+// records its start and end (s_memrealtime, 100 MHz) and its key range [beg, end), read back with
+// rsort_lab_wg_times. Absent from the library.
 #ifdef RSORT_WG_TIMES
-__device__ unsigned long long g_wg_times[4][256][4];
+__device__ unsigned long long g_wg_times[8][2048][4];
 __device__ unsigned long long g_wg_htimes[4][256][4];
 #define RS_WG_T0 const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();
-#define RS_WG_TREC(TAB, B, E)                                                                     \
+#define RS_WG_TREC(TAB, SLOT, NB, B, E)                                                           \
     do {                                                                                          \
         __syncthreads();                                                                          \
-        if (threadIdx.x == 0 && blockIdx.x < 256) {                                               \
-            unsigned long long *p_ = TAB[(a.shift / 8u) & 3u][blockIdx.x];                         \
+        if (threadIdx.x == 0 && blockIdx.x < (NB)) {                                              \
+            unsigned long long *p_ = TAB[SLOT][blockIdx.x];                                       \
             p_[0] = wg_t0_;                                                                       \
             p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
             p_[2] = (B);                                                                          \
             p_[3] = (E);                                                                          \
         }                                                                                         \
     } while (0)
-#define RS_WG_T1 RS_WG_TREC(g_wg_times, cbeg, cend)
-#define RS_WG_TH1 RS_WG_TREC(g_wg_htimes, beg, end)
+#define RS_WG_T1 RS_WG_TREC(g_wg_times, (a.shift / BITS) & 7u, 2048u, cbeg, cend)
+#define RS_WG_TH1 RS_WG_TREC(g_wg_htimes, (a.shift / 8u) & 3u, 256u, beg, end)
 #else
 #define RS_WG_T0
 #define RS_WG_T1
@@ -2964,7 +2965,7 @@ hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t
 #ifdef RSORT_WG_TIMES
 extern "C" __attribute__((visibility("default"))) int rsort_lab_wg_times(unsigned long long *host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsort::g_wg_times), sizeof(rsort::g_wg_times)) == hipSuccess &&
-                   hipMemcpyFromSymbol(host + 4 * 256 * 4, HIP_SYMBOL(rsort::g_wg_htimes), sizeof(rsort::g_wg_htimes)) ==
+                   hipMemcpyFromSymbol(host + 8 * 2048 * 4, HIP_SYMBOL(rsort::g_wg_htimes), sizeof(rsort::g_wg_htimes)) ==
                        hipSuccess
                ? 0
                : 6;

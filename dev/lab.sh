@@ -237,6 +237,17 @@ wgt)
     rm -f gpurun_out/wgt_lib.so
     cat gpurun_out/wgt.log
     ;;
+wgtk)
+    # the same lab build: per-workgroup start / end of every pass of one sort (args: e.g. --k 4 --log2n 26)
+    cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
+    cp dev/var_wgt.so cuda.radixsort_amd/librsort.so
+    timeout -k 10 240 python dev/wgtimes_lab.py --dist uniform "$@" >> gpurun_out/wgtk.log 2>&1
+    rc=$?
+    cp gpurun_out/wgt_lib.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/wgt_lib.so
+    cat gpurun_out/wgtk.log
+    stop_unless_ok $rc wgtk
+    ;;
 wgth)
     # the same lab build: per-workgroup durations of the joint-count histograms (Zipf, uniform keys;
     # WGT_VAR picks another lab build dev/var_$WGT_VAR.so, WGT_DISTS the distributions)

@@ -22,6 +22,7 @@ ap.add_argument("--dist", default="zipf")
 ap.add_argument("--log2n", type=int, default=29)
 ap.add_argument("--pass", dest="pss", type=int, default=1)
 ap.add_argument("--pairs", action="store_true")
+ap.add_argument("--k", type=int, default=8, help="digit bits (k = 4: C2's eight passes; no chunk contents)")
 ap.add_argument("--dump", default="", help="write every chunk of the pass as CSV (us, keys, top digit share, H)")
 ap.add_argument("--hist", action="store_true",
                 help="also the joint-count histograms (passes 0 and 2) and what the slowest pass-2 chunks hold")
@@ -43,16 +44,18 @@ if a.pairs:
     rs.gen_iota(vals, 0)
 out = rs.empty_u32(n)
 vout = rs.empty_u32(n) if a.pairs else None
-p = rs.plan(n, 8, a.pairs)
+p = rs.plan(n, a.k, a.pairs)
 ws = rs.workspace(p.workspace_bytes)
 for _ in range(3):
-    rs.sort_device(keys, out, 8, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
+    rs.sort_device(keys, out, a.k, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
 torch.cuda.synchronize()
-both = np.zeros((2, 4, 256, 4), dtype=np.uint64)
+both = np.zeros(8 * 2048 * 4 + 4 * 256 * 4, dtype=np.uint64)
 assert fn(both.ctypes.data) == 0
-buf, hbuf = both[0], both[1]
-print("modes", rs.group_flags(p, ws))
-for ps in range(4):
+nch = min(p.num_chunks, 2048)
+buf = both[: 8 * 2048 * 4].reshape(8, 2048, 4)[:, :nch]
+hbuf = both[8 * 2048 * 4:].reshape(4, 256, 4)
+print("modes", rs.group_flags(p, ws), "chunks", p.num_chunks)
+for ps in range(p.passes):
     t0, t1, cb, ce = (buf[ps, :, i].astype(np.int64) for i in range(4))
     dur = (t1 - t0) * 10 / 1e3  # 100 MHz ticks -> us
     start = (t0 - t0.min()) * 10 / 1e3
@@ -60,7 +63,10 @@ for ps in range(4):
     print(f"pass {ps}: wall {((t1.max() - t0.min()) * 10 / 1e3):8.1f} us  per-wg dur min/med/max "
           f"{dur.min():7.1f} {np.median(dur):7.1f} {dur.max():7.1f}  start spread {start.max():5.1f} us  "
           f"keys/chunk min/max {size.min()} {size.max()}  us per Mkey min/med/max "
-          f"{(dur / size * 1e6).min():.1f} {np.median(dur / size * 1e6):.1f} {(dur / size * 1e6).max():.1f}")
+          f"{(dur / size * 1e6).min():.1f} {np.median(dur / size * 1e6):.1f} {(dur / size * 1e6).max():.1f}  "
+          f"end spread {((t1.max() - t1.min()) * 10 / 1e3):5.1f} us")
+if a.k != 8:
+    sys.exit(0)
 # the chunks of the pass asked for: what they hold (its input = the previous pass's output: the keys
 # stably sorted by the lower digits, computed here)
 ps = a.pss
