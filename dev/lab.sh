@@ -237,6 +237,26 @@ wgt)
     rm -f gpurun_out/wgt_lib.so
     cat gpurun_out/wgt.log
     ;;
+c2tpc)
+    # C2 (2^26 keys, k = 4) with tiles_per_chunk 16 (the plan's default: one resident wave of
+    # workgroups), 8 and 4 (two and four waves: the dispatcher balances the later waves), raw next-digit
+    # tables and tail scans (RSORT_NX_TAIL=1), alternating twice
+    for rep in 1 2; do
+        for tpc in ${C2_TPCS:-16 8 4}; do
+            for tail in 0 1; do
+                RSORT_NX_TAIL=$tail timeout -k 10 120 python bench.py --keys 67108864 --k 4 --tiles-per-chunk $tpc \
+                    --steps 20 --warmup 5 --no-cpu --no-vendor --no-e2e --configs "" > gpurun_out/c2tpc.json 2> gpurun_out/c2tpc.err
+                stop_unless_ok $? "c2 tpc=$tpc tail=$tail" > /dev/null
+                python3 - "$tpc" "$tail" <<'PY'
+import json, sys
+d = json.loads(open("gpurun_out/c2tpc.json").read().strip().splitlines()[-1])
+print("tpc %2s tail %s: %.4f ms/sort  scatter %.4f ms/pass  chunks %d  verified %s" % (sys.argv[1], sys.argv[2],
+      d["ms_per_step"], d["roofline"]["avg_launch_ms"], d["config"]["num_chunks"], d["verified"]))
+PY
+            done
+        done
+    done
+    ;;
 wgtk)
     # the same lab build: per-workgroup start / end of every pass of one sort (args: e.g. --k 4 --log2n 26)
     cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
