@@ -55,8 +55,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--keys", "--n", dest="n", type=int, default=1 << 30, help="keys per GPU")
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--dist", choices=["uniform", "zipf", "equal"], default="uniform",
-                    help="key distribution (equal: every key the same, the clustered extreme)")
+    ap.add_argument("--dist", choices=["uniform", "zipf", "equal", "hot", "zipf12"], default="uniform",
+                    help="key distribution (equal: every key the same, the clustered extreme; hot: a quarter of "
+                         "the keys one value at random positions, the rest uniform; zipf12: Zipf s=1.2)")
     ap.add_argument("--pairs", action="store_true")
     ap.add_argument("--rank", choices=["match", "split"], default="match")
     ap.add_argument("--tiles-per-chunk", type=int, default=0)
@@ -88,6 +89,11 @@ def parse():
                          "reported in the line's `configs` block ('' for none; N=1 only): " + ", ".join(CONFIGS))
     ap.add_argument("--configs-n", type=int, default=0, help="override every config's key count (tests)")
     ap.add_argument("--configs-reps", type=int, default=7, help="timed sorts per config (median)")
+    ap.add_argument("--configs-cpu-n", type=int, default=1 << 26,
+                    help="keys of each config's CPU-baseline row (a prefix of its input; 0: none)")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="--gpus N without a launcher: seconds before the N ranks are killed and this command "
+                         "exits non-zero (0: 300 s + 60 s per 2^30 keys over all ranks)")
     return ap.parse_args()
 
 
@@ -138,6 +144,53 @@ def _cpu_model():
     except OSError:
         pass
     return "host CPU"
+
+
+def config_cpu_row(c, host_keys, host_vals, reps):
+    """BASELINE.md §3's CPU row beside a GPU configuration: the reference's Baseline1 sortByHost
+    (oracle/_ref, kind "reference") on a prefix of the config's own keys at its k -- or, for pairs
+    (Baseline1 has no payload), the oracle's pairs port of the same loop (kind "port") -- ONE thread
+    pinned to one core, median of `reps` runs."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _util  # test/bench infrastructure (never the product path)
+    k = c["k"]
+    x = np.ascontiguousarray(host_keys)
+    ko = np.empty_like(x)
+    if host_vals is not None:
+        v = np.ascontiguousarray(host_vals)
+        vo = np.empty_like(v)
+        kind, what = "port", "the oracle's pairs restatement of Baseline1 (Baseline1.cu:15-64 carrying a payload)"
+
+        def run():
+            _util.oracle().oracle_sort_pairs_by_host(_util._ptr(x), _util._ptr(v), x.size, _util._ptr(ko),
+                                                     _util._ptr(vo), k)
+    else:
+        ref = _util.ref_lib()
+        kind = "reference" if ref is not None else "port"
+        what = "Baseline1 sortByHost" + (" (the reference's own code, oracle/_ref)" if ref is not None else
+                                         " (the oracle's restatement)")
+
+        def run():
+            if ref is not None:
+                ref.ref_sort_by_host(_util._ptr(x), x.size, _util._ptr(ko), k)
+            else:
+                _util.oracle().oracle_sort_by_host(_util._ptr(x), x.size, _util._ptr(ko), k)
+    old = _pin_one_core()
+    try:
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            run()
+            ts.append(time.perf_counter() - t0)
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
+    med = float(np.median(ts))
+    return {"value": round(x.size / med / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": kind,
+            "sample": f"{x.size} {c['dist']} u32 {'key+value pairs' if host_vals is not None else 'keys'} "
+                      f"(a prefix of this config's input), k={k}, median of {reps} runs of {what}, one thread "
+                      f"pinned to one core of {_cpu_model()}",
+            "ms_per_sort": round(med * 1e3, 2)}
 
 
 def cpu_baseline(host_keys, n, k, reps, dist, rows):
@@ -250,14 +303,21 @@ def gen_keys(n, dist, seed, dev):
         rs.gen_uniform(keys, seed)
     elif dist == "equal":
         keys.fill_(0x1234567)
+    elif dist == "hot":
+        rs.gen_uniform(keys, seed)
+        sel = rs.empty_u32(n, dev)
+        rs.gen_uniform(sel, seed ^ 0x5A5A5A5A5A)
+        keys[(sel & 3) == 0] = 0xC0FFEE
+        del sel
     else:
         sys.path.insert(0, str(ROOT / "tests"))
         from _util import zipf_cdf_u32  # the workload's CDF table (data, not the oracle)
-        rs.gen_zipf(keys, rs.from_numpy_u32(zipf_cdf_u32(), dev), seed)
+        cdf = zipf_cdf_u32(s=1.2) if dist == "zipf12" else zipf_cdf_u32()
+        rs.gen_zipf(keys, rs.from_numpy_u32(cdf, dev), seed)
     return keys
 
 
-def run_config(name, c, dev, reps, n_override=0):
+def run_config(name, c, dev, reps, n_override=0, cpu_n=0, cpu_reps=3):
     """One BASELINE configuration, device-resident like the headline: ms per sort = the median of
     `reps` back-to-back sorts, each between two HIP events on the library's stream (torch's current
     stream); the scatter kernel's average launch time from HIP events around every scatter launch
@@ -312,19 +372,44 @@ def run_config(name, c, dev, reps, n_override=0):
            "scatter_kernels": rs.scatter_kernels_used(reset=True),
            "plan_check": rs.plan_check(p, ws),
            "verified": bool(fp_out == fp_in and desc == 0)}
+    if cpu_n > 0:
+        m = min(cpu_n, n)
+        res["cpu_baseline"] = config_cpu_row(c, rs.to_numpy_u32(keys[:m]),
+                                             rs.to_numpy_u32(vals[:m]) if vals is not None else None, cpu_reps)
     del keys, vals, out, vout, ws
     torch.cuda.empty_cache()
     return res
 
 
+def visible_gpus() -> int:
+    """GPUs this process may use, without touching HIP: HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES when set, else the render nodes (/dev/dri/renderD*) of the machine."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip()])
+    return len(list(Path("/dev/dri").glob("renderD*")))
+
+
+def launch_timeout(a) -> float:
+    """Seconds the N ranks of a self-launched run may take: --launch-timeout, else 300 s (a fresh box's
+    first `import torch`, RCCL setup) + 60 s per 2^30 keys over all ranks (the CPU baseline and the
+    configs run at N = 1 only)."""
+    return a.launch_timeout if a.launch_timeout > 0 else 300.0 + 60.0 * a.n * a.gpus / (1 << 30)
+
+
 def self_launch(a) -> int:
     """`--gpus N` (N > 1) started plainly, without torch.distributed.run: start the N ranks as ONE
     child `python -m torch.distributed.run` (127.0.0.1, a free port) running this same command line,
-    and return its exit code. This process never initialises HIP (device_count() does not) and never
+    in a process group of its own, and return its exit code. The run is bounded: past launch_timeout
+    the whole group is killed (SIGTERM, then SIGKILL) and this exits 124 with a message, so a stalled
+    rank (a peer that died, a collective that never completes) ends the command instead of hanging it.
+    This process never initialises HIP (it counts GPUs from the environment / device nodes) and never
     re-execs; the children inherit stdout, so rank 0's JSON line is this command's output."""
+    import signal
     import socket
     import subprocess
-    visible = torch.cuda.device_count()  # (counts devices without initialising HIP on this image)
+    visible = visible_gpus()
     if os.environ.get("RSORT_BENCH_BACKEND", "") != "gloo" and visible < a.gpus:
         print(f"bench.py: --gpus {a.gpus} but {visible} GPU(s) visible (RSORT_BENCH_BACKEND=gloo rehearses "
               f"N ranks on fewer GPUs)", file=sys.stderr)
@@ -336,8 +421,32 @@ def self_launch(a) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (RCCL over dmabuf IPC on these hosts)
+    limit = launch_timeout(a)
+    env["RSORT_BENCH_TIMEOUT"] = str(int(limit))  # (the ranks bound their own collectives below it)
     sys.stdout.flush()
-    return subprocess.run(cmd, env=env).returncode
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait(timeout=limit)
+    except subprocess.TimeoutExpired:
+        print(f"bench.py: the {a.gpus} ranks did not finish within {limit:.0f} s (a stalled or dead rank); "
+              f"killing process group {proc.pid}", file=sys.stderr, flush=True)
+        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                proc.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        return 124
+    except BaseException:
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        raise
 
 
 def _template_args(name):
@@ -428,12 +537,23 @@ def main():
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         # control plane (barriers, the time max, the RCCL id) on gloo; the keys move over RCCL:
-        # rsort_u32_multi's own communicator (c) or torch's nccl process group (torch)
+        # rsort_u32_multi's own communicator (c) or torch's nccl process group (torch). Every wait is
+        # bounded: gloo's collectives and RCCL's steps (rsort_set_comm_timeout) time out below the
+        # launcher's limit, so a stalled peer ends the run with an error instead of a hang
+        import datetime
+        limit = float(os.environ.get("RSORT_BENCH_TIMEOUT", "600"))
+        to = datetime.timedelta(seconds=max(30.0, limit - 60.0))
+        rs.set_comm_timeout(int(max(30.0, limit - 90.0) * 1000))
         with stdout_to_stderr():
             if a.dist_impl == "torch" and not rehearsal:
-                dist.init_process_group("nccl", device_id=dev)
+                dist.init_process_group("nccl", device_id=dev, timeout=to)
             else:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=to)
+    # TEST HOOK (tests/test_gpu_bench.py): this rank stalls before its first collective, as a dead peer
+    # would; its peers then wait in that collective until the timeouts above or the launcher end them
+    if os.environ.get("RSORT_BENCH_STALL_RANK", "") == str(rank) and world > 1:
+        print(f"bench.py: rank {rank} stalls (RSORT_BENCH_STALL_RANK)", file=sys.stderr, flush=True)
+        time.sleep(10 ** 6)
     rs.set_rank_algo(rs.RANK_SPLIT if a.rank == "split" else rs.RANK_MATCH)
     rs.set_group_chunks(not a.no_group_chunks)
     if a.primitives:
@@ -629,7 +749,8 @@ def main():
         torch.cuda.empty_cache()
         configs = {}
         for name in [x.strip() for x in a.configs.split(",") if x.strip()]:
-            configs[name] = run_config(name, CONFIGS[name], dev, a.configs_reps, a.configs_n)
+            configs[name] = run_config(name, CONFIGS[name], dev, a.configs_reps, a.configs_n,
+                                       0 if (a.no_cpu or rank != 0) else a.configs_cpu_n, a.cpu_reps)
 
     cpu = None
     if rank == 0 and host_keys is not None and not a.no_cpu:
@@ -672,6 +793,8 @@ def main():
             "dtype": "u32",
             "data": {"uniform": "synthetic (splitmix64 uniform u32, seed 0x5EED, generated in HBM)",
                      "zipf": "synthetic (Zipf s=1.0 over 2^20 ranks, key=fmix32(rank))",
+                     "zipf12": "synthetic (Zipf s=1.2 over 2^20 ranks, key=fmix32(rank))",
+                     "hot": "synthetic (uniform u32, a quarter of the positions set to 0x00C0FFEE)",
                      "equal": "synthetic (every key 0x01234567)"}[a.dist],
             "config": {"workload": f"sort {n} {'key+value pairs' if a.pairs else 'uint32 keys'} per GPU, "
                                    f"k={a.k} ({p.passes} passes), {a.dist}"

@@ -27,6 +27,7 @@ namespace {
 constexpr int kVersion = 100;  // 0.1.0
 std::atomic<int> g_rank_algo{RSORT_RANK_MATCH};
 std::atomic<int> g_group_chunks{1};
+std::atomic<int> g_table_fault{0};  // rsort_inject_table_fault (tests)
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -104,11 +105,11 @@ int device_cus() {
     return c;
 }
 
-// log2 of the smallest k = 4 keys-only sort on 1024-thread line tiles (default 28; RSORT_K4_LINES_LG in
-// the environment for A/B runs)
+// log2 of the smallest k = 4 keys-only sort on 1024-thread line tiles (default 28; RSORT_K4_LINES_LG
+// under RSORT_LAB=1 for A/B runs)
 int k4_lines_lg() {
     static const int v = [] {
-        const char *e = getenv("RSORT_K4_LINES_LG");
+        const char *e = lab_env("RSORT_K4_LINES_LG");
         const int x = e ? atoi(e) : 0;
         return (x >= 16 && x <= 32) ? x : 28;
     }();
@@ -147,20 +148,20 @@ bool joint_plan(const rsort_plan &p) {
            (geom_from_shape(p.threads, p.tile_keys, p.pairs) == (p.pairs ? kGeomLinesPairs : kGeomLines));
 }
 
-// RSORT_CUT_WEIGHTS=0 in the environment: cut plans with equal key counts per chunk (A/B runs)
+// RSORT_CUT_WEIGHTS=0 under RSORT_LAB=1: cut plans with equal key counts per chunk (A/B runs)
 bool cut_weights() {
     static const bool v = [] {
-        const char *e = getenv("RSORT_CUT_WEIGHTS");
+        const char *e = lab_env("RSORT_CUT_WEIGHTS");
         return !(e != nullptr && e[0] == '0');
     }();
     return v;
 }
 
-// RSORT_NX_TAIL=1 in the environment: next-digit plans scan each pass's table in its last workgroup
+// RSORT_NX_TAIL=1 under RSORT_LAB=1: next-digit plans scan each pass's table in its last workgroup
 // (the round-3 scheme) instead of every workgroup of the next pass summing the raw counts (A/B runs)
 bool nx_tail() {
     static const bool v = [] {
-        const char *e = getenv("RSORT_NX_TAIL");
+        const char *e = lab_env("RSORT_NX_TAIL");
         return e != nullptr && e[0] != '\0' && e[0] != '0';
     }();
     return v;
@@ -462,7 +463,8 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // next-digit plans: every pass after the first derives its offsets from the raw counts the pass
     // before added (three tables in rotation: read / added into / cleared for the pass after next),
     // instead of the last workgroup of each pass scanning them (RSORT_NX_TAIL=1: that older way)
-    const bool rawt = nextc && !nx_tail();
+    // (raw tables only up to kRawTableMaxChunks chunks: each workgroup reads the whole table)
+    const bool rawt = nextc && !nx_tail() && p.num_chunks <= kRawTableMaxChunks;
     uint32_t *const rot[3] = {c.table, c.table2, c.table3};
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
@@ -501,6 +503,11 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
                              (nxt && !rawt) ? tab : nullptr, (nextc && (nxt || rawt)) ? c.done : nullptr, cl,
                              rawt, clr)))
             return st;
+        // test hook: corrupt the raw table pass 1 reads (its total is then not n: every pass-1 workgroup
+        // writes nothing and records the failure for rsort_plan_check / RSORT_ERR_CHECK)
+        if (i == 0 && rawt && nxt && g_table_fault.load() &&
+            hipMemsetD32Async((hipDeviceptr_t)nxt, 0xFFFFFFFFu, 1, s) != hipSuccess)
+            return RSORT_ERR_HIP;
         sk = dk;
         sv = dv;
     }
@@ -747,6 +754,22 @@ int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flag
     flags[1] = (int)h[1];
     return RSORT_OK;
 }
+
+int rsort_plan_features(const rsort_plan *plan) {
+    if (check_plan(plan) != RSORT_OK) return -RSORT_ERR_ARG;
+    const rsort_plan &p = *plan;
+    const bool atomic = internal_rank(g_rank_algo.load()) == kRankAtomic;
+    const bool on = g_group_chunks.load() != 0 && atomic;
+    int f = 0;
+    if (joint_plan(p) && on) f |= RSORT_FEAT_GROUPS;
+    if (next_plan(p) && on) {
+        f |= RSORT_FEAT_NEXT_DIGIT;
+        f |= (!nx_tail() && p.num_chunks <= kRawTableMaxChunks) ? RSORT_FEAT_RAW_TABLES : RSORT_FEAT_TAIL_SCAN;
+    }
+    return f;
+}
+
+int rsort_inject_table_fault(int enable) { return g_table_fault.exchange(enable ? 1 : 0); }
 
 int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream) {
     if (!plan || !flags || !d_workspace) return RSORT_ERR_ARG;

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace rsort {
 
@@ -220,5 +221,17 @@ void profile_pause(int delta);
 // Workspace check words (next-digit plans): done[kDoneErr] is set when a tail scan found a table
 // whose total is not n even after an agent-scope acquire and a second sweep.
 constexpr uint32_t kDoneErr = 1;
+// Raw next-digit tables (every workgroup of a pass sums the whole R x C table for its own starts) cost
+// O(R x C) reads per workgroup, O(R x C^2) per pass: only plans of at most this many chunks (about one
+// resident wave: C2 has 1024) take them; larger ones keep the tail scan (DESIGN §8 measured
+// 2048 chunks 1.155 vs 1.088 ms, 4096 chunks 1.578 vs 1.207 ms per C2 sort against tail scans).
+constexpr int64_t kRawTableMaxChunks = 1280;
+// Lab switches (A/B runs, dev/lab.sh): the library reads getenv(name) only when RSORT_LAB=1 is set
+// too, so a shipped library picks its plans from n, k and the device alone. nullptr otherwise.
+inline const char *lab_env(const char *name) {
+    const char *lab = getenv("RSORT_LAB");
+    if (lab == nullptr || lab[0] != '1') return nullptr;
+    return getenv(name);
+}
 
 }  // namespace rsort

@@ -380,7 +380,8 @@ struct Digit {
 // Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup (the first 2048 of a
 // pass; slot = shift / BITS) and every joint-count histogram workgroup (g_wg_htimes, slot = shift / 8)
 // records its start and end (s_memrealtime, 100 MHz) and its key range [beg, end), read back with
-// rsort_lab_wg_times. Absent from the library.
+// rsort_lab_wg_times; the upper halves of the range words hold where it ran: HW_ID (hwreg 4: cu 11:8,
+// sh 12, se 15:13) over beg, XCC_ID (hwreg 20) over end. Absent from the library.
 #ifdef RSORT_WG_TIMES
 __device__ unsigned long long g_wg_times[8][2048][4];
 __device__ unsigned long long g_wg_htimes[4][256][4];
@@ -390,10 +391,12 @@ __device__ unsigned long long g_wg_htimes[4][256][4];
         __syncthreads();                                                                          \
         if (threadIdx.x == 0 && blockIdx.x < (NB)) {                                              \
             unsigned long long *p_ = TAB[SLOT][blockIdx.x];                                       \
+            const unsigned long long hw_ = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   \
+            const unsigned long long xc_ = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  \
             p_[0] = wg_t0_;                                                                       \
             p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
-            p_[2] = (B);                                                                          \
-            p_[3] = (E);                                                                          \
+            p_[2] = (unsigned long long)(B) | (hw_ << 32);                                        \
+            p_[3] = (unsigned long long)(E) | (xc_ << 32);                                        \
         }                                                                                         \
     } while (0)
 #define RS_WG_T1 RS_WG_TREC(g_wg_times, (a.shift / BITS) & 7u, 2048u, cbeg, cend)
@@ -810,8 +813,12 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_down(ScanArgs a) {
 // exactly once, so its total must be `expect` (= n): the sum sweep checks that, and on a mismatch
 // (a late or stale line -- never observed) the workgroup takes the agent-scope acquire fence and
 // sums again; a second mismatch sets done[kDoneErr] -- so a visibility failure is repaired, or
-// recorded where rsort_plan_check reads it (the sort itself still returns RSORT_OK: a caller that
-// must know asks rsort_plan_check after the sort, as rsort.h says). All threads must call it.
+// recorded where rsort_plan_check reads it. rsort.h is the contract: the stream-ordered device entries
+// return RSORT_OK (they do not wait for the device) and a caller that must know asks rsort_plan_check;
+// the host entries (rsort_u32*, which wait anyway) read the word and return RSORT_ERR_CHECK. Since round
+// 4 this tail scan runs only under RSORT_NX_TAIL=1 (RSORT_LAB) or for plans with more chunks than the
+// raw tables take (kRawTableMaxChunks); the default is raw_offsets, which checks the same total per
+// workgroup. All threads must call it.
 template <int THREADS>
 __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t *done, uint32_t *s_ws,
                           uint32_t *s_flag, uint32_t expect) {
@@ -1684,6 +1691,18 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         // ... and, in slot 0, iff this lane's tile position is not before the chunk (head)
         const bool h0 = base >= head;
         head = 0;
+#ifdef RSORT_PRIO_ROT
+        // lab: several workgroups per CU (C2: 4) end in dispatch order (the older wins the CU's
+        // arbitration); rotating the wave priority per tile gives each the lead in turn
+        if constexpr (THREADS == 256) {
+            switch ((uint32_t)(((tb - cbeg) / T) + (c >> 8)) & 3u) {
+                case 0: __builtin_amdgcn_s_setprio(0); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                default: __builtin_amdgcn_s_setprio(3); break;
+            }
+        }
+#endif
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
         for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
@@ -2512,11 +2531,11 @@ static void *reg_pairs() {
     return fn;
 }
 
-// Pairs with k = 7, 8 write 128-B lines through rs_scatter_pairs; RSORT_PAIRS64=1 in the environment
+// Pairs with k = 7, 8 write 128-B lines through rs_scatter_pairs; RSORT_PAIRS64=1 under RSORT_LAB=1
 // selects rs_scatter_lines' 64-B-line pairs kernel instead (A/B measurements, dev/lab.sh).
 static bool pairs_lines64() {
     static const bool v = [] {
-        const char *e = getenv("RSORT_PAIRS64");
+        const char *e = lab_env("RSORT_PAIRS64");
         return e != nullptr && e[0] != '\0' && e[0] != '0';
     }();
     return v;
@@ -2844,9 +2863,14 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
             cl = reg_lines<8, PT, PK, kLineKeysPairs, true, kDigitShift, 2, 1>();
 
     }
+    // digit-group chunks, next-digit counts and raw tables exist only in the whole-line kernels: any
+    // other kernel would read the unscanned counts (or the group bounds) as offsets -- refuse, never
+    // sort wrongly
+    const bool lines = is_line_kernel(fn);
+    if ((a.raw_table || a.next_table != nullptr || a.bounds != nullptr) && !lines) return hipErrorInvalidValue;
     ScatterArgs copy = a;
     if (cl == nullptr) copy.cl_select = nullptr;  // no clustered variant: the plain kernel does the pass
-    if (is_line_kernel(fn)) {
+    if (lines) {
         // whole-line kernels write cache lines: positions count from kout's 128-B-aligned base, the
         // slots before kout are masked like any chunk's leading slots (values: the same shift; the
         // caller checked (vout - kout) % 16 == 0, so vout's base stays 16-B aligned)

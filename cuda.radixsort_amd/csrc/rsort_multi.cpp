@@ -25,6 +25,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "rsort.h"
@@ -198,14 +199,79 @@ void side_release(SideStream *x) {
 }
 
 // ------------------------------------------------------------------------------ RCCL transport
+// Every RCCL step is bounded: RCCL itself never times out, so a peer that died or
+// never joined would leave this rank's kernels spinning and its host waiting forever. Each step's
+// calls are completed (a non-blocking communicator returns ncclInProgress until they are), then the
+// step's stream work is polled to completion; past the deadline, or on an asynchronous RCCL error,
+// the communicator is aborted (ncclCommAbort also stops its kernels) and RSORT_ERR_COMM returned.
+std::atomic<int> g_comm_timeout_ms{300000};  // rsort_set_comm_timeout
+std::mutex g_aborted_mu;
+std::vector<void *> g_aborted;  // communicators a timeout aborted (rsort_rccl_comm_destroy skips them)
+
+bool comm_aborted(ncclComm_t c) {
+    std::lock_guard<std::mutex> g(g_aborted_mu);
+    return std::find(g_aborted.begin(), g_aborted.end(), (void *)c) != g_aborted.end();
+}
+
+int comm_abort(ncclComm_t c) {
+    {
+        std::lock_guard<std::mutex> g(g_aborted_mu);
+        if (std::find(g_aborted.begin(), g_aborted.end(), (void *)c) != g_aborted.end()) return RSORT_ERR_COMM;
+        g_aborted.push_back((void *)c);
+    }
+    (void)ncclCommAbort(c);
+    return RSORT_ERR_COMM;
+}
+
+using Clock = std::chrono::steady_clock;
+
+// r == ncclInProgress (a non-blocking communicator): poll until the call has completed
+ncclResult_t nb_complete(ncclComm_t c, ncclResult_t r, Clock::time_point deadline) {
+    while (r == ncclInProgress) {
+        if (Clock::now() > deadline) return ncclInProgress;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (ncclCommGetAsyncError(c, &r) != ncclSuccess) return ncclInternalError;
+    }
+    return r;
+}
+
+// the step's calls returned `r`; now wait (bounded) for its work on `s`
+int rccl_finish(ncclComm_t c, ncclResult_t r, hipStream_t s, Clock::time_point deadline) {
+    r = nb_complete(c, r, deadline);
+    if (r != ncclSuccess) return comm_abort(c);
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return RSORT_ERR_HIP;
+    int st = hipEventRecord(ev, s) == hipSuccess ? RSORT_OK : RSORT_ERR_HIP;
+    for (int spin = 0; st == RSORT_OK; ++spin) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {
+            st = RSORT_ERR_HIP;
+            break;
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress) ||
+            Clock::now() > deadline) {
+            st = comm_abort(c);
+            break;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    (void)hipEventDestroy(ev);
+    return st;
+}
+
+Clock::time_point comm_deadline() { return Clock::now() + std::chrono::milliseconds(g_comm_timeout_ms.load()); }
+
 struct RcclCtx {
     ncclComm_t comm;
 };
 
 int rccl_allgather(void *ctx, const void *d_send, void *d_recv, size_t bytes, void *stream) {
     ncclComm_t comm = static_cast<RcclCtx *>(ctx)->comm;
-    return ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, (hipStream_t)stream) == ncclSuccess ? RSORT_OK
-                                                                                                     : RSORT_ERR_COMM;
+    const Clock::time_point dl = comm_deadline();
+    return rccl_finish(comm, ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, (hipStream_t)stream),
+                       (hipStream_t)stream, dl);
 }
 
 int rccl_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void *const *d_recv,
@@ -214,10 +280,11 @@ int rccl_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void
     int world = 0, me = 0;
     if (ncclCommCount(comm, &world) != ncclSuccess || ncclCommUserRank(comm, &me) != ncclSuccess) return RSORT_ERR_COMM;
     hipStream_t s = (hipStream_t)stream;
+    const Clock::time_point dl = comm_deadline();
     // every call inside the group is checked; the group is always closed (an open group would
     // leave the communicator unusable), and the first failure is returned
     ncclResult_t first = ncclGroupStart();
-    if (first != ncclSuccess) return RSORT_ERR_COMM;
+    if (first != ncclSuccess) return comm_abort(comm);
     for (int p = 0; p < world; ++p) {
         if (p == me) continue;
         if (send_bytes[p]) {
@@ -230,8 +297,8 @@ int rccl_exchange(void *ctx, void *const *d_send, const size_t *send_bytes, void
         }
     }
     const ncclResult_t e = ncclGroupEnd();
-    if (first == ncclSuccess) first = e;
-    return first == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM;
+    if (first == ncclSuccess || first == ncclInProgress) first = e;
+    return rccl_finish(comm, first, s, dl);
 }
 
 // ------------------------------------------------------------------------------ loopback transport
@@ -397,7 +464,8 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     if (workspace_bytes < m.control_bytes) return RSORT_ERR_WORKSPACE;
     // Every other local failure is carried to the peers in the next all-gather (a status word per
     // rank) and returned by every rank together -- the lowest rank's status first -- instead of
-    // leaving the peers waiting in a collective this rank never joins (RCCL has no timeout).
+    // leaving the peers waiting in a collective this rank never joins (a rank that dies instead is
+    // caught by the RCCL transport's bounded waits: rccl_finish).
     int local = RSORT_OK;
     if (k_bits < kMinBits || k_bits > kMaxBits) local = RSORT_ERR_BITS;
     else if (!sizes_ok) local = RSORT_ERR_SIZE;
@@ -682,6 +750,7 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
                     uint32_t *d_vals_out, int64_t capacity, int64_t *out_n, int64_t *out_offset, int k_bits,
                     void *nccl_comm, void *d_workspace, size_t workspace_bytes, void *stream) {
     if (!nccl_comm) return RSORT_ERR_ARG;
+    if (comm_aborted((ncclComm_t)nccl_comm)) return RSORT_ERR_COMM;  // (a timeout aborted it earlier)
     RcclCtx ctx{(ncclComm_t)nccl_comm};
     int world = 0, me = 0;
     if (ncclCommCount(ctx.comm, &world) != ncclSuccess || ncclCommUserRank(ctx.comm, &me) != ncclSuccess)
@@ -689,6 +758,41 @@ int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, u
     rsort_transport tr{&ctx, world, me, rccl_allgather, rccl_exchange};
     return multi_sort(d_keys, d_vals, n, d_keys_out, d_vals_out, capacity, out_n, out_offset, k_bits, &tr,
                       d_workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int rsort_rccl_unique_id(void *id128) {
+    if (!id128) return RSORT_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == 128, "NCCL_UNIQUE_ID_BYTES");
+    return ncclGetUniqueId(static_cast<ncclUniqueId *>(id128)) == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM;
+}
+
+int rsort_rccl_comm_init(void **comm, int world, int rank, const void *id128, int timeout_ms) {
+    if (!comm || !id128 || world < 1 || rank < 0 || rank >= world) return RSORT_ERR_ARG;
+    *comm = nullptr;
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof(id));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;  // returns at once; setup runs in the background and is polled below
+    ncclComm_t c = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&c, world, id, rank, &cfg);
+    if (c == nullptr) return RSORT_ERR_COMM;
+    const int ms = timeout_ms > 0 ? timeout_ms : g_comm_timeout_ms.load();
+    r = nb_complete(c, r, Clock::now() + std::chrono::milliseconds(ms));
+    if (r != ncclSuccess) return comm_abort(c);  // (a peer never joined, or setup failed)
+    *comm = c;
+    return RSORT_OK;
+}
+
+int rsort_rccl_comm_destroy(void *comm) {
+    if (!comm) return RSORT_ERR_ARG;
+    if (comm_aborted((ncclComm_t)comm)) return RSORT_OK;  // released by the abort
+    return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM;
+}
+
+int rsort_set_comm_timeout(int timeout_ms) {
+    const int old = g_comm_timeout_ms.load();
+    if (timeout_ms > 0) g_comm_timeout_ms.store(timeout_ms);
+    return old;
 }
 
 int rsort_multi_inject_failure(int rank, int stage, int status) {

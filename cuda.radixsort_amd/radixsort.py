@@ -181,6 +181,8 @@ SIGNATURES = {
     "rsort_group_flags": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_lane_order_probe": ([], _int),
     "rsort_plan_check": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
+    "rsort_plan_features": ([_PP], _int),
+    "rsort_inject_table_fault": ([_int], _int),
     "rsort_scatter_kernels_used": ([ctypes.c_char_p, _sz, _int], _sz),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
@@ -203,6 +205,10 @@ SIGNATURES = {
     "rsort_set_multi_options": ([_int], _int),
     "rsort_multi_exchange_rounds": ([_i64, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
     "rsort_multi_set_profiling": ([_int], _int),
+    "rsort_rccl_unique_id": ([_vp], _int),
+    "rsort_rccl_comm_init": ([ctypes.POINTER(ctypes.c_void_p), _int, _int, _vp, _int], _int),
+    "rsort_rccl_comm_destroy": ([_vp], _int),
+    "rsort_set_comm_timeout": ([_int], _int),
     "rsort_multi_inject_failure": ([_int, _int, _int], _int),
     "rsort_multi_last_stats": ([ctypes.POINTER(MultiStats)], _int),
     "rsort_host_transport_wrap": ([ctypes.POINTER(HostTransportFns), ctypes.POINTER(Transport)], _int),
@@ -373,6 +379,27 @@ def group_flags(p: Plan, ws, stream=None) -> list[int]:
     return [int(flags[0]), int(flags[1])]
 
 
+FEAT_GROUPS, FEAT_NEXT_DIGIT, FEAT_RAW_TABLES, FEAT_TAIL_SCAN = 1, 2, 4, 8
+
+
+def plan_features(p: Plan) -> int:
+    """rsort_plan_features: the carried-histogram scheme a sort with plan `p` takes (FEAT_* bits)."""
+    f = int(_lib().rsort_plan_features(ctypes.byref(p)))
+    if f < 0:
+        raise RSortError(-f, "rsort_plan_features")
+    return f
+
+
+@contextmanager
+def table_fault():
+    """TEST HOOK (rsort_inject_table_fault): raw-table sorts corrupt the table pass 1 reads."""
+    old = _lib().rsort_inject_table_fault(1)
+    try:
+        yield
+    finally:
+        _lib().rsort_inject_table_fault(old)
+
+
 def plan_check(p: Plan, ws, stream=None) -> int:
     """The on-device self-checks of the last sort with plan `p` and workspace `ws`
     (rsort_plan_check; synchronises the stream): 0 = all passed."""
@@ -435,54 +462,48 @@ def scatter_kernel_name(p: Plan, out_aligned16: bool = True) -> str:
         ((p.threads, p.tile_keys) == (1024, 8192) and p.pairs and 5 <= p.k_bits <= 8) or \
         ((p.threads, p.tile_keys) == (256, 4096) and not p.pairs and 3 <= p.k_bits <= 4)
     if lines and out_aligned16 and get_rank_algo() == RANK_MATCH and lane_order_probe() == 1:
-        # RSORT_PAIRS64=1 (A/B runs) makes the library's dispatch take the 64-B-line pairs kernel
-        pairs64 = os.environ.get("RSORT_PAIRS64", "") not in ("", "0")
+        # RSORT_PAIRS64=1 under RSORT_LAB=1 (A/B runs) makes the library's dispatch take the 64-B-line
+        # pairs kernel
+        pairs64 = os.environ.get("RSORT_LAB", "") == "1" and os.environ.get("RSORT_PAIRS64", "") not in ("", "0")
         return "rs_scatter_pairs" if p.pairs and p.k_bits >= 7 and not pairs64 else "rs_scatter_lines"
     return "rs_scatter"
 
 
 # ---------------------------------------------------------------- multi-GPU over RCCL (C ABI)
-class NcclUniqueId(ctypes.Structure):
-    _fields_ = [("internal", ctypes.c_char * 128)]  # NCCL_UNIQUE_ID_BYTES (rccl.h)
-
-
-_rccl = None
-
-
-def _rccl_lib():
-    global _rccl
-    if _rccl is None:
-        _rccl = ctypes.CDLL("librccl.so.1", mode=ctypes.RTLD_GLOBAL)
-        _rccl.ncclGetUniqueId.argtypes = [ctypes.POINTER(NcclUniqueId)]
-        _rccl.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, NcclUniqueId, ctypes.c_int]
-        _rccl.ncclCommDestroy.argtypes = [ctypes.c_void_p]
-    return _rccl
+NCCL_UNIQUE_ID_BYTES = 128
 
 
 def rccl_unique_id() -> bytes:
-    uid = NcclUniqueId()
-    if _rccl_lib().ncclGetUniqueId(ctypes.byref(uid)) != 0:
-        raise RSortError(10, "ncclGetUniqueId")
-    return ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))  # raw: the id holds NUL bytes
+    """rsort_rccl_unique_id: made on one rank, sent to the others out of band."""
+    buf = ctypes.create_string_buffer(NCCL_UNIQUE_ID_BYTES)
+    _check(_lib().rsort_rccl_unique_id(buf), "rsort_rccl_unique_id")
+    return buf.raw  # (raw: the id holds NUL bytes)
+
+
+def set_comm_timeout(ms: int) -> int:
+    """rsort_set_comm_timeout: how long one RCCL step of the multi-GPU sort may take before the
+    communicator is aborted (RSORT_ERR_COMM instead of a hang); returns the old value."""
+    return int(_lib().rsort_set_comm_timeout(int(ms)))
 
 
 class RcclComm:
-    """An RCCL communicator for rsort_u32_multi (one rank per GPU; the current device)."""
+    """An RCCL communicator for rsort_u32_multi (one rank per GPU; the current device), set up
+    non-blocking by rsort_rccl_comm_init: a peer that never joins ends in RSortError (status 10,
+    RSORT_ERR_COMM) after `timeout_ms` (default: the library's communicator timeout) instead of a
+    hang. After any RSORT_ERR_COMM from a sort the communicator may have been aborted; close() knows."""
 
-    def __init__(self, world: int, rank: int, uid: bytes):
-        u = NcclUniqueId()
-        if len(uid) != ctypes.sizeof(u):
+    def __init__(self, world: int, rank: int, uid: bytes, timeout_ms: int = 0):
+        if len(uid) != NCCL_UNIQUE_ID_BYTES:
             raise ValueError("RCCL unique id must be 128 bytes")
-        ctypes.memmove(ctypes.addressof(u), uid, len(uid))
+        buf = ctypes.create_string_buffer(bytes(uid), NCCL_UNIQUE_ID_BYTES)
         self.handle = ctypes.c_void_p()
-        r = _rccl_lib().ncclCommInitRank(ctypes.byref(self.handle), int(world), u, int(rank))
-        if r != 0:
-            raise RSortError(10, f"ncclCommInitRank (ncclResult {r})")
+        _check(_lib().rsort_rccl_comm_init(ctypes.byref(self.handle), int(world), int(rank), buf, int(timeout_ms)),
+               "rsort_rccl_comm_init")
         self.world, self.rank = world, rank
 
     def close(self):
         if self.handle:
-            _rccl_lib().ncclCommDestroy(self.handle)
+            _lib().rsort_rccl_comm_destroy(self.handle)
             self.handle = ctypes.c_void_p()
 
 

@@ -7,6 +7,7 @@
 #
 #   round            pytest -m gpu (all) + the default bench line (what the driver runs at round end)
 #   tests [-k EXPR]  pytest -m gpu, optionally filtered
+#   nodes NODE...    pytest -m gpu on these files / node ids only (-s; LAB_TAG names gpurun_out/nodes_TAG.log)
 #   pairs            the pairs tests + C4 and Zipf keys through bench.py, then C4 with the 64-B-line
 #                    pairs kernel (RSORT_PAIRS64=1) for A/B on the same box
 #   pairslab         dev/pairs_lab: one pairs pass, 64-B vs 128-B kernels, per-phase cycles
@@ -29,6 +30,12 @@
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
 #   dist             kernel trace of the multi-GPU step on one rank (bench.py --dist-path)
+#   ceiling          dev/ceiling_lab: copy / read / write ceilings (policies, grids, shapes) and per-workgroup
+#                    copy rates by XCC (gpurun_out/ceiling.jsonl; profiles/r05_ceilings.json)
+#   wgtx             (WGTX_ARGS="..." for one run) dev/var_wgt.so: per-workgroup scatter rates of repeated sorts against XCC, physical CU
+#                    and chunk (dev/wgtimes_lab.py --reps)
+#   cutw             ADVICE r4: cost-weighted cut plans vs equal-count ones (RSORT_LAB=1 RSORT_CUT_WEIGHTS=0) on
+#                    Zipf s=1 at 2^28 / 2^30, Zipf s=1.2 and "hot" keys at 2^30, keys and pairs, alternating twice
 #   profiles TAG     the committed profile set: run_profiles.sh for C3, Zipf keys, C4 and C2 (TAG,
 #                    TAG_zipf, TAG_c4, TAG_c2), then kernel traces of the one-rank multi-GPU step, the
 #                    default (direct sort) and the whole protocol (--dist-full)
@@ -76,6 +83,13 @@ tests)
         > gpurun_out/lab_tests.log 2>&1
     ok_or_stop $? pytest
     grep -E "passed|failed|FAILED|Error" gpurun_out/lab_tests.log | tail -n 20
+    ;;
+nodes)
+    # pytest on the given test files / node ids only (LAB_TAG names the log), -s so prints are kept
+    timeout -k 10 1000 python -u -m pytest -v -s --maxfail 8 --timeout 600 --timeout-method thread -m gpu "$@" \
+        > gpurun_out/nodes_${LAB_TAG:-x}.log 2>&1
+    ok_or_stop $? "pytest nodes"
+    grep -E "PASSED|FAILED|ERROR|SKIPPED|passed|failed" gpurun_out/nodes_${LAB_TAG:-x}.log | tail -n 30
     ;;
 pairs)
     timeout -k 10 600 python -u -m pytest tests -m gpu -v -k "pairs or clustered or cut_plan or group" \
@@ -283,6 +297,54 @@ wgth)
     cp gpurun_out/wgt_lib.so cuda.radixsort_amd/librsort.so
     rm -f gpurun_out/wgt_lib.so
     cat gpurun_out/wgth.log
+    ;;
+ceiling)
+    timeout -k 10 240 dev/ceiling_lab 30 10 > gpurun_out/ceiling.jsonl 2> gpurun_out/ceiling.err
+    stop_unless_ok $? ceiling
+    grep -v chunk_records gpurun_out/ceiling.jsonl | tail -n 30
+    ;;
+wgtx)
+    cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
+    cp dev/var_wgt.so cuda.radixsort_amd/librsort.so
+    rc=0
+    set -- "--dist uniform --log2n 30 --reps 4" "--dist uniform --log2n 26 --k 4 --reps 4" "--dist zipf --log2n 30 --reps 3"
+    [ -n "$WGTX_ARGS" ] && set -- "$WGTX_ARGS"
+    for args in "$@"; do
+        timeout -k 10 240 python dev/wgtimes_lab.py $args >> gpurun_out/wgtx.log 2>&1
+        rc=$?
+        echo "[lab] wgtx $args rc=$rc"
+        [ $rc -eq 0 ] || break
+    done
+    cp gpurun_out/wgt_lib.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/wgt_lib.so
+    cat gpurun_out/wgtx.log
+    stop_unless_ok $rc wgtx
+    ;;
+cutw)
+    : > gpurun_out/cutw.log
+    for rep in 1 2; do
+        for args in "--dist zipf --keys 268435456" "--dist zipf" "--dist zipf12" "--dist hot" "--dist zipf --pairs" \
+                    "--dist hot --pairs"; do
+            for w in 1 0; do
+                if [ $w = 1 ]; then
+                    timeout -k 10 200 python bench.py $args --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e --configs "" \
+                        > gpurun_out/cutw.json 2> gpurun_out/cutw.err
+                else
+                    RSORT_LAB=1 RSORT_CUT_WEIGHTS=0 timeout -k 10 200 python bench.py $args --steps 10 --warmup 3 --no-cpu \
+                        --no-vendor --no-e2e --configs "" > gpurun_out/cutw.json 2> gpurun_out/cutw.err
+                fi
+                stop_unless_ok $? "cutw $args w=$w" > /dev/null
+                python3 - "$args" "$w" >> gpurun_out/cutw.log <<'PY'
+import json, sys
+d = json.loads(open("gpurun_out/cutw.json").read().strip().splitlines()[-1])
+print("%-32s weights=%s %8.3f ms/sort  scatter %.4f ms/pass  hist %.3f  modes %s  %s" % (sys.argv[1], sys.argv[2],
+      d["ms_per_step"], d["roofline"]["avg_launch_ms"], d["phases_ms_per_step"]["histogram"],
+      d["config"]["group_chunk_modes"], d["verified"]))
+PY
+            done
+        done
+    done
+    cat gpurun_out/cutw.log
     ;;
 prof)
     tag=$1

@@ -189,14 +189,35 @@ RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace,
                                 void *stream);
 /* After a sort with `plan` and `d_workspace` has completed on `stream`: *flags = 0 when every
  * on-device self-check of that sort passed; bit 0 = a k = 3, 4 pass found the next-digit table it
- * reads not holding n keys (the pass then wrote nothing; with RSORT_NX_TAIL=1: a tail scan found it
- * so even after an acquire fence and a second sweep) -- the sort's output is then not trustworthy. Synchronises the stream. The sort entry points are stream-ordered and do not
+ * reads not holding n keys (the pass then wrote nothing; with RSORT_FEAT_TAIL_SCAN: a tail scan found it
+ * so even after an acquire fence and a second sweep) -- the sort's output is then not trustworthy.
+ * Synchronises the stream. The sort entry points are stream-ordered and do not
  * wait for the device, so they CANNOT return this check: they return RSORT_OK for such a sort, and
  * this call is the only way to learn of it. rsort_u32_device / rsort_u32_pairs_device use the plan
  * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace. The host
  * entries (rsort_u32, rsort_u32_ex, rsort_u32_pairs) wait for the device anyway: they read the check
  * themselves and return RSORT_ERR_CHECK for such a sort. Never observed failing. */
 RSORT_API int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream);
+/* Which carried-histogram scheme a sort with `plan` takes under the current process settings
+ * (rsort_set_rank_algo, rsort_set_group_chunks), for outputs the whole-line kernels can write (any
+ * 4-B-aligned keys output): a bitmask, or -RSORT_ERR_ARG for an invalid plan.
+ *   RSORT_FEAT_GROUPS       k = 8, 256 chunks: digit-group chunks on the odd passes
+ *   RSORT_FEAT_NEXT_DIGIT   k = 3, 4 keys: next-digit counts (only pass 0 reads keys for a histogram)
+ *   RSORT_FEAT_RAW_TABLES   ... each pass after the first derives its starts from the raw counts in
+ *                           every workgroup (plans of at most 1280 chunks: the per-workgroup sum
+ *                           reads the whole R x C table)
+ *   RSORT_FEAT_TAIL_SCAN    ... the last workgroup of each pass scans the next table instead (plans
+ *                           with more chunks, e.g. a small tiles_per_chunk) */
+#define RSORT_FEAT_GROUPS 1
+#define RSORT_FEAT_NEXT_DIGIT 2
+#define RSORT_FEAT_RAW_TABLES 4
+#define RSORT_FEAT_TAIL_SCAN 8
+RSORT_API int rsort_plan_features(const rsort_plan *plan);
+/* TEST HOOK (never set in production): enable != 0 makes every raw-table sort (RSORT_FEAT_RAW_TABLES)
+ * corrupt one word of the table pass 1 reads, as a lost update would; that pass's workgroups then
+ * find the table not holding n keys, write nothing, and record it: rsort_plan_check reports bit 0 and
+ * the host entries return RSORT_ERR_CHECK. Process-wide; returns the previous setting. */
+RSORT_API int rsort_inject_table_fault(int enable);
 /* The scatter kernel instantiations this library has launched since the last reset, ';'-joined
  * into buf (at most len - 1 characters and a NUL); returns the full length. reset != 0 clears the
  * record. A k = 8 digit-group sort launches a plain and a clustered-input kernel for each pass
@@ -322,17 +343,36 @@ RSORT_API int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, in
  * Errors: a failure on one rank before the exchange (bad k_bits / sizes / pointers, a workspace
  * too small, a device error in sampling, sample sort or partition) travels in a status word of the
  * next all-gather, and EVERY rank returns the lowest rank's status together -- no rank is left
- * waiting in a collective (RCCL has no timeout). Only a transport that cannot run at all (NULL
+ * waiting in a collective (a rank that dies instead is caught by the RCCL timeout below). Only a transport that cannot run at all (NULL
  * transport or workspace, a workspace smaller than the collectives' control buffers) returns at
  * once on that rank. Failures in or after the exchange (the exchange itself, the local sort) are
  * the failing rank's own. */
 RSORT_API size_t rsort_multi_workspace_size(int64_t n, int64_t capacity, int k_bits, int pairs, int world);
 /* Over an RCCL communicator (`nccl_comm` is an ncclComm_t; RCCL result codes are all checked,
- * RSORT_ERR_COMM on failure). */
+ * RSORT_ERR_COMM on failure). Every RCCL call is bounded: the sort waits for each collective and
+ * exchange round to complete (host-polled), and when one has not completed within the communicator
+ * timeout (rsort_set_comm_timeout) -- a peer that died or never joined -- or RCCL reports an
+ * asynchronous error, it aborts the communicator (ncclCommAbort) and returns RSORT_ERR_COMM. The
+ * communicator is then gone: do not use or destroy it again (rsort_rccl_comm_destroy knows it). */
 RSORT_API int rsort_u32_multi(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n,
                               uint32_t *d_keys_out, uint32_t *d_vals_out, int64_t capacity,
                               int64_t *out_n, int64_t *out_offset, int k_bits, void *nccl_comm,
                               void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* RCCL communicators with bounded setup (replaces ncclGetUniqueId / ncclCommInitRank for the
+ * callers of rsort_u32_multi): the id (NCCL_UNIQUE_ID_BYTES = 128 bytes) is made on one rank and
+ * sent to the others out of band; init creates the rank's communicator on the current device,
+ * non-blocking (ncclCommInitRankConfig, blocking = 0), and polls it until it is ready -- or, after
+ * timeout_ms (<= 0: the rsort_set_comm_timeout value), aborts it and returns RSORT_ERR_COMM, so a
+ * peer that never joins cannot hang this rank. destroy: ncclCommDestroy, or nothing for a
+ * communicator a timeout already aborted. */
+RSORT_API int rsort_rccl_unique_id(void *id128);
+RSORT_API int rsort_rccl_comm_init(void **comm, int world, int rank, const void *id128, int timeout_ms);
+RSORT_API int rsort_rccl_comm_destroy(void *comm);
+/* How long one RCCL step of rsort_u32_multi (a collective, an exchange round, the communicator's
+ * setup) may take before the communicator is aborted: default 300000 ms. Process-wide; returns the
+ * previous value; values <= 0 leave it unchanged. */
+RSORT_API int rsort_set_comm_timeout(int timeout_ms);
 
 /* Options of rsort_u32_multi* (process-wide; returns the previous flags):
  *  RSORT_MULTI_OVERLAP  every rank's key range is cut in two at a sampled quantile (the planning

@@ -23,7 +23,8 @@ def run_bench(*args):
 
 def test_bench_headline_contract():
     d = run_bench("--steps", "2", "--warmup", "1", "--keys", str(1 << 24), "--cpu-n", str(1 << 20), "--cpu-reps", "1",
-                  "--cpu-rows", "18,24", "--configs-n", str((1 << 22) + 5), "--configs-reps", "5")
+                  "--cpu-rows", "18,24", "--configs-n", str((1 << 22) + 5), "--configs-reps", "5",
+                  "--configs-cpu-n", str(1 << 20))
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "vendor", "end_to_end"):
         assert k in d, k
@@ -49,6 +50,14 @@ def test_bench_headline_contract():
         assert 0 < c["scatter"]["frac"] < 1 and c["scatter"]["bytes_per_key"] == (16 if c["pairs"] else 8), name
         assert c["scatter_kernels"], name
     assert d["configs"]["c4"]["pairs"] and d["configs"]["c2"]["k_bits"] == 4
+    # BASELINE.md §3's CPU row beside every configuration: Baseline1 at the config's k
+    # (C2: k = 4), the oracle's pairs port for C4 (Baseline1 carries no payload)
+    for name, c in d["configs"].items():
+        cb = c["cpu_baseline"]
+        assert cb["cores"] == 1 and cb["value"] > 0 and f"k={c['k_bits']}" in cb["sample"], (name, cb)
+        assert str(1 << 20) in cb["sample"]
+    assert d["configs"]["c2"]["cpu_baseline"]["kind"] in ("reference", "port")
+    assert d["configs"]["c4"]["cpu_baseline"]["kind"] == "port" and "pairs" in d["configs"]["c4"]["cpu_baseline"]["sample"]
 
 
 def test_bench_group_chunks_reported():
@@ -166,3 +175,34 @@ def test_bench_plain_gpus4_rehearsal_ragged():
     # one key everywhere: the equal-keys bucket is cut across the ranks evenly
     outs = d["multi"]["keys_out_per_rank"]
     assert max(outs) - min(outs) <= 0.05 * sum(outs) / 4 + 64, outs
+
+
+def test_bench_gpus2_stalled_rank_ends_with_an_error():
+    """the first real N-GPU run must not hang or end without a word. One rehearsal rank
+    stalls before its first collective (RSORT_BENCH_STALL_RANK, a test hook), as a dead peer would:
+    `bench.py --gpus 2` must exit non-zero within its launch timeout with a message, and leave no
+    process of the run behind (the ranks and the launcher are one process group, killed on expiry)."""
+    import os
+    import time
+    import uuid
+    psutil = pytest.importorskip("psutil")
+    tag = uuid.uuid4().hex
+    env = dict(os.environ, RSORT_BENCH_BACKEND="gloo", RSORT_BENCH_STALL_RANK="1", RSORT_BENCH_TAG=tag)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--keys", str(1 << 20), "--no-cpu", "--launch-timeout", "60"], capture_output=True, text=True,
+                       timeout=200, cwd=str(ROOT), env=env)
+    el = time.monotonic() - t0
+    assert r.returncode != 0, r.stdout[-1000:]
+    assert el < 60 + 20 + 30, el  # (limit + the kill's grace periods + interpreter start)
+    assert "stalls" in r.stderr or "did not finish" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]  # no line from a failed run
+    time.sleep(2)
+    left = []
+    for p in psutil.process_iter():
+        try:
+            if p.environ().get("RSORT_BENCH_TAG") == tag:
+                left.append((p.pid, p.cmdline()[:4]))
+        except (psutil.AccessDenied, psutil.NoSuchProcess, psutil.ZombieProcess):
+            continue
+    assert not left, left

@@ -365,3 +365,104 @@ def test_next_digit_counts_chunk_geometries(tpc):
     d_out = rs.empty_u32(n)
     rs.sort_device(rs.from_numpy_u32(x), d_out, 4, plan_=p)
     assert np.array_equal(rs.to_numpy_u32(d_out), oracle_sort(x, 4))
+
+
+# ------------------------------------------------------------------ raw tables vs tail scans
+@pytest.mark.parametrize("n,tpc,want_raw", [((1 << 22) + 9, 1, True), ((1 << 23) + 9, 1, False), ((1 << 24) + 5, 2, False),
+                                            ((1 << 26), 0, True)])
+def test_raw_tables_only_for_small_chunk_counts(n, tpc, want_raw):
+    """Raw next-digit tables make every workgroup read the whole R x C table (O(R C^2) per pass), so a
+    plan takes them only up to 1280 chunks; a small tiles_per_chunk (2^23 keys in 4096-key chunks:
+    2049 chunks) keeps the tail scan. rsort_plan_features says which ran; the output is the oracle's
+    either way, and the sort's self-check is clean."""
+    p = rs.plan(n, 4, False, tpc)
+    f = rs.plan_features(p)
+    assert f & rs.FEAT_NEXT_DIGIT, f
+    assert bool(f & rs.FEAT_RAW_TABLES) == want_raw and bool(f & rs.FEAT_TAIL_SCAN) == (not want_raw), (p.num_chunks, f)
+    assert (p.num_chunks <= 1280) == want_raw
+    x = uniform_keys(n, seed=n ^ tpc)
+    ws = rs.workspace(p.workspace_bytes)
+    d_out = rs.empty_u32(n)
+    rs.sort_device(rs.from_numpy_u32(x), d_out, 4, ws=ws, plan_=p)
+    assert rs.plan_check(p, ws) == 0
+    got = rs.to_numpy_u32(d_out)
+    if n <= (1 << 24) + 5:
+        assert np.array_equal(got, oracle_sort(x, 4))
+    else:
+        assert np.array_equal(got, np.sort(x))
+
+
+def test_plan_features_of_the_default_plans():
+    assert rs.plan_features(rs.plan(1 << 30, 8)) == rs.FEAT_GROUPS
+    assert rs.plan_features(rs.plan(1 << 26, 4)) == rs.FEAT_NEXT_DIGIT | rs.FEAT_RAW_TABLES
+    assert rs.plan_features(rs.plan(1 << 20, 11)) == 0
+    with rs.group_chunks(False):
+        assert rs.plan_features(rs.plan(1 << 26, 4)) == 0
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_corrupted_raw_table_is_reported(k):
+    """the raw-table failure path. With the test hook one word of the table pass 1 reads
+    is corrupted: that pass's workgroups see a total that is not n, write nothing and record it, so
+    rsort_plan_check reports bit 0 (device entry) and the host entry returns RSORT_ERR_CHECK (11).
+    The hook cleared, the same sorts are correct again."""
+    n = (1 << 20) + 33
+    x = uniform_keys(n, seed=k)
+    p = rs.plan(n, k)
+    assert rs.plan_features(p) & rs.FEAT_RAW_TABLES
+    ws = rs.workspace(p.workspace_bytes)
+    d_out = rs.empty_u32(n)
+    with rs.table_fault():
+        rs.sort_device(rs.from_numpy_u32(x), d_out, k, ws=ws, plan_=p)
+        assert rs.plan_check(p, ws) == 1
+        with pytest.raises(rs.RSortError) as e:
+            rs.sortByDevice(x, n, np.empty_like(x), k)
+        assert e.value.status == 11
+    rs.sort_device(rs.from_numpy_u32(x), d_out, k, ws=ws, plan_=p)
+    assert rs.plan_check(p, ws) == 0
+    want = oracle_sort(x, k)
+    assert np.array_equal(rs.to_numpy_u32(d_out), want)
+    y = np.empty_like(x)
+    rs.sortByDevice(x, n, y, k)
+    assert np.array_equal(y, want)
+
+
+_LAB_SNIPPET = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import radixsort as rs
+from _util import oracle_sort, uniform_keys, zipf_keys
+out = []
+for k, gen, n in ((3, uniform_keys, (1 << 21) + 3), (4, zipf_keys, (1 << 21) + 7), (8, zipf_keys, 1 << 24)):
+    x = gen(n, seed=k)
+    p = rs.plan(n, k)
+    ws = rs.workspace(p.workspace_bytes)
+    d = rs.empty_u32(n)
+    rs.sort_device(rs.from_numpy_u32(x), d, k, ws=ws, plan_=p)
+    ok = np.array_equal(rs.to_numpy_u32(d), oracle_sort(x, k)) and rs.plan_check(p, ws) == 0
+    out.append(f"k{k}:{int(ok)}:{rs.plan_features(p)}:{rs.group_flags(p, ws) if k == 8 else ''}")
+print(" ".join(out))
+'''
+
+
+@pytest.mark.parametrize("env,feat4", [({"RSORT_LAB": "1", "RSORT_NX_TAIL": "1", "RSORT_CUT_WEIGHTS": "0"}, 2 | 8),
+                                       ({"RSORT_NX_TAIL": "1", "RSORT_CUT_WEIGHTS": "0"}, 2 | 4)])
+def test_lab_switches_in_a_subprocess(env, feat4):
+    """The A/B switches are read once per process, and only under RSORT_LAB=1 (VERDICT r4 #8): with
+    it, k = 3, 4 sorts take the tail scans (features) and the Zipf k = 8 sort equal-count cut plans;
+    without it the same variables change nothing. Both sort correctly (ADVICE r4)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    e = dict(os.environ)
+    e.pop("RSORT_LAB", None)
+    e.update(env)
+    r = subprocess.run([sys.executable, "-c", _LAB_SNIPPET, str(root / "cuda.radixsort_amd"), str(root / "tests")],
+                       capture_output=True, text=True, timeout=240, env=e)
+    assert r.returncode == 0, r.stderr[-2000:]
+    parts = r.stdout.split()
+    assert [x.split(":")[1] for x in parts] == ["1", "1", "1"], r.stdout
+    assert parts[0].split(":")[2] == str(feat4) and parts[1].split(":")[2] == str(feat4), r.stdout
+    assert parts[2].split(":")[3] == "[2, 2]", r.stdout  # Zipf keys: cut plans on passes 1 and 3

@@ -507,3 +507,42 @@ def test_c_multi_2gib_message():
     finally:
         rs.set_multi_options(old)
         comm.close()
+
+
+_INIT_SNIPPET = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import torch
+import radixsort as rs
+torch.cuda.set_device(0)
+uid = rs.rccl_unique_id()
+t0 = time.monotonic()
+try:
+    rs.RcclComm(2, 0, uid, timeout_ms=5000)  # rank 1 never joins
+    print("JOINED")
+except rs.RSortError as e:
+    print(f"STATUS {e.status} {time.monotonic() - t0:.1f}")
+"""
+
+
+def test_rccl_init_deadline_when_a_peer_never_joins():
+    """the communicator is set up non-blocking (ncclCommInitRankConfig, blocking = 0)
+    and polled; rank 0 of a world-2 communicator whose rank 1 never joins gets RSORT_ERR_COMM after
+    its 5-s deadline (the setup is aborted) instead of waiting forever. In a subprocess, so a hang in
+    RCCL's abort could only fail this test."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", _INIT_SNIPPET, str(PKG)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith(("STATUS", "JOINED"))]
+    assert line and line[0].startswith("STATUS 10"), r.stdout[-1000:]
+    assert 4.0 <= float(line[0].split()[2]) < 60.0, line
+
+
+def test_rccl_comm_timeout_setting():
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    old = rs.set_comm_timeout(1234)
+    try:
+        assert rs.set_comm_timeout(0) == 1234  # (<= 0 leaves it unchanged)
+    finally:
+        rs.set_comm_timeout(old)
