@@ -214,6 +214,8 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
     if (joint_plan(*p)) {
         ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
+        ws += align256((size_t)kJointBins * 4);               // work-stealing claims (joint counts)
+        ws += align256((size_t)p->table_entries * 4);         // ... and the stolen keys' digit counts
         ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
         ws += align256((size_t)kPlanWords * 4);               // cut plan
         ws += align256((size_t)kPieceSlots * kJointBins * 4); // its piece counts
@@ -238,7 +240,8 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done, *table3;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *claims, *steal, *bounds, *plan, *pcounts, *table2, *done,
+        *table3;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -259,6 +262,10 @@ Carve carve(const rsort_plan &p, void *ws) {
     if (joint_plan(p)) {
         c.joint = (uint32_t *)q;
         q += align256((size_t)kJointBins * kJointBins * 4);
+        c.claims = (uint32_t *)q;  // (claims and steal follow the joint counts: one memset clears all three)
+        q += align256((size_t)kJointBins * 4);
+        c.steal = (uint32_t *)q;
+        q += align256((size_t)p.table_entries * 4);
         c.bounds = (uint32_t *)q;
         q += align256((size_t)2 * kBoundsWords * 4);
         c.plan = (uint32_t *)q;
@@ -285,7 +292,7 @@ Carve carve(const rsort_plan &p, void *ws) {
 // adds runs of equal pairs once (rs_histogram's run path), so pass 3 gets its own cut plan too.
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                        uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
-                       uint32_t *pcounts, hipStream_t s, bool zero_joint) {
+                       uint32_t *pcounts, hipStream_t s, bool zero_joint, uint32_t *claims, uint32_t *steal) {
     HistArgs a{};
     a.keys = keys;
     a.table = table;
@@ -297,10 +304,14 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     a.split = 1;
     a.joint = joint;
     a.joint_enable = enable;
+    a.claims = claims;
+    a.steal = steal;
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
-    // the first joint count of a sort clears the counts; a later one finds them cleared by the
-    // copy-mode histogram that used them (or, where that pass fell back, is disabled by `enable`)
-    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess)
+    // the first joint count of a sort clears the counts and the work-stealing state (contiguous); a
+    // later one finds them cleared by the copy-mode histogram / the scan that used them (or, where that
+    // pass fell back, is disabled by `enable`)
+    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)((char *)steal - (char *)joint) + (size_t)p.table_entries * 4, s) !=
+                          hipSuccess)
         return RSORT_ERR_HIP;
     if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
     // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
@@ -354,9 +365,15 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
 }
 
 int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr,
-            uint32_t *done = nullptr, const Carve *cut = nullptr, const uint32_t *group_flag = nullptr) {
+            uint32_t *done = nullptr, const Carve *cut = nullptr, const uint32_t *group_flag = nullptr,
+            const Carve *stolen = nullptr) {
     ScanArgs a{};
     a.done = done;
+    if (stolen != nullptr) {
+        // after a work-stealing joint count: its stolen counts join the table
+        a.steal = stolen->steal;
+        a.claims = stolen->claims;
+    }
     if (cut != nullptr) {
         // a digit-group pass: under a cut plan the scan assembles the table first
         a.group_flag = group_flag;
@@ -482,7 +499,8 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
-                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0)))
+                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0, c.claims,
+                                         c.steal)))
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
@@ -493,7 +511,8 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // raw tables: no scan at all, the histogram cleared the next table), every later table by the
         // previous scatter's last workgroup (raw tables: by every workgroup of the pass itself)
         if (!(nextc && i > 0) && !rawt &&
-            (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds)))
+            (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds,
+                          count_joint ? &c : nullptr)))
             return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
         // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the

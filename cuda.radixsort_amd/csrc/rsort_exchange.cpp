@@ -187,7 +187,10 @@ int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, int64_t *rou
     limit = std::max<int64_t>(limit, 64);
     const int64_t r0 = (max_message + limit - 1) / limit;  // rounds at the limit
     int64_t p = (max_message + r0 - 1) / r0;               // equal pieces, <= limit
-    p = std::max<int64_t>(64, p / 64 * 64);                // a multiple of 64, rounded down
+    // a multiple of 64: rounded up where that stays within the limit (r0 rounds; rounding down made a
+    // one-round message of 2^27 + 6 keys take a second round of 6 keys), else down (never above it)
+    const int64_t up = (p + 63) / 64 * 64;
+    p = up <= limit ? up : std::max<int64_t>(64, p / 64 * 64);
     *piece = p;
     *rounds = (max_message + p - 1) / p;
     return RSORT_OK;

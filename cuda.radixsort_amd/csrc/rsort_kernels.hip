@@ -428,13 +428,19 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     constexpr uint32_t RS = R / 2 + 1;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t *s_sp = s_j + R * RS;
+    // work stealing (a.claims): stolen keys' digit counts, per victim (s_st) and in total (s_stot)
+    __shared__ uint32_t s_st[R], s_stot[R];
+    __shared__ uint32_t s_claim, s_victim;
     const uint32_t t = threadIdx.x;
     RS_WG_T0
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
+    for (uint32_t i = t; i < R; i += THREADS) s_st[i] = s_stot[i] = 0;
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
     // add inc (<= 64) to the 16-bit counter of pair (d, e); the add that takes it to 2^15 moves 2^15
-    // to the row's spill word and to the global count (the counter stays below 2^15 + 64)
+    // to the row's spill word and to the global count (the counter stays below 2^15 + 64). Keys of a
+    // stolen unit also count their digit in s_st (they are not this chunk's).
+    bool stolen = false;
     auto add_pair = [&](uint32_t d, uint32_t e, uint32_t inc) {
         const uint32_t wi = d * RS + (e >> 1), sh = (e & 1u) << 4;
         const uint32_t before = (atomicAdd(&s_j[wi], inc << sh) >> sh) & 0xFFFFu;
@@ -443,6 +449,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             atomicAdd(&s_sp[d], 0x8000u);
             atomicAdd(&a.joint[e * R + d], 0x8000u);
         }
+        if (stolen) atomicAdd(&s_st[d], inc);
     };
     auto add = [&](uint32_t x) { add_pair((x >> s0) & (R - 1u), (x >> s1) & (R - 1u), 1u); };
     // Clustered input (runs of equal keys: sorted or duplicate-heavy data, and every pass after a cut
@@ -465,59 +472,138 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             add_pair(pr & 0xFFu, pr >> 8, end - lane_id());
         }
     };
+    // keys [beg, end) (beg 16-B aligned when a.vec) into the joint counts
+    auto count_keys = [&](uint64_t beg, uint64_t end) {
+        uint64_t tail = beg;
+        if (a.vec) {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
+            const uint32_t nvec = (uint32_t)((end - beg) / 4);
+            constexpr int U = 4;
+            for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
+                u32x4 q[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t v = v0 + u * THREADS;
+                    ok[u] = v < nvec;
+                    q[u] = ok[u] ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
+                }
+                // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
+                if (wave_count(__ballot(ok[0] && pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (ok[u]) {
+                            add(q[u].x);
+                            add(q[u].y);
+                            add(q[u].z);
+                            add(q[u].w);
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (ok[u]) {
+                            add_run(q[u].x);
+                            add_run(q[u].y);
+                            add_run(q[u].z);
+                            add_run(q[u].w);
+                        }
+                    }
+                }
+            }
+            tail = beg + (uint64_t)nvec * 4;
+        }
+        for (uint64_t i = tail + t; i < end; i += THREADS) add(a.keys[i]);
+    };
     const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
     const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
     const uint64_t beg = min(cbeg + sub * part, cend);
     const uint64_t end = min(beg + part, cend);
-    uint64_t tail = beg;
-    if (a.vec) {
-        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
-        const uint32_t nvec = (uint32_t)((end - beg) / 4);
-        constexpr int U = 4;
-        for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
-            u32x4 q[U];
-            bool ok[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t v = v0 + u * THREADS;
-                ok[u] = v < nvec;
-                q[u] = ok[u] ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
+    if (a.claims == nullptr || S != 1) {
+        count_keys(beg, end);
+    } else {
+        // Work stealing (the counts do not depend on which workgroup adds them; round 5): a chunk is
+        // units of kStealUnit keys; its first half is its own workgroup's, the second half goes to
+        // whoever claims it first (a.claims[chunk], one global add per unit, issued a unit ahead). A
+        // workgroup done with its chunk claims units of the chunks with the most units left. Stolen
+        // keys' digit counts go to a.steal[d][chunk] (added into the table by the scan) and are taken
+        // out of this chunk's row sums; the joint counts are global anyway. Skewed (clustered) passes
+        // end with their slowest chunks instead of waiting for them (Zipf pass 2: 271 vs ~240 us/Mkey).
+        const uint32_t nc = a.num_chunks;
+        auto units_of = [&](uint32_t v) {
+            const uint64_t vb = (uint64_t)v * a.chunk_keys, ve = min(vb + a.chunk_keys, a.n);
+            return (uint32_t)(ve > vb ? (ve - vb + kStealUnit - 1) / kStealUnit : 0);
+        };
+        auto unit_range = [&](uint32_t v, uint32_t u, uint64_t &ub, uint64_t &ue) {
+            const uint64_t vb = (uint64_t)v * a.chunk_keys, ve = min(vb + a.chunk_keys, a.n);
+            ub = min(vb + (uint64_t)u * kStealUnit, ve);
+            ue = min(ub + kStealUnit, ve);
+        };
+        const uint32_t nu = units_of(c), own = nu / 2;
+        // the first half: no claims
+        count_keys(cbeg, min(cbeg + (uint64_t)own * kStealUnit, cend));
+        // the second half and then the other chunks' second halves: claim unit by unit (the next
+        // claim's global add is issued before the current unit is counted)
+        uint32_t v = c;
+        uint32_t pend = 0u;  // thread 0: the claim in flight for chunk v
+        if (t == 0) pend = atomicAdd(&a.claims[v], 1u);
+        for (;;) {
+            __syncthreads();  // (s_claim / s_victim reuse)
+            if (t == 0) s_claim = pend;
+            __syncthreads();
+            const uint32_t u = s_claim, vu = units_of(v), vo = vu / 2;
+            if (vo + u < vu) {
+                if (t == 0) pend = atomicAdd(&a.claims[v], 1u);  // the next one, in flight
+                uint64_t ub, ue;
+                unit_range(v, vo + u, ub, ue);
+                stolen = v != c;
+                count_keys(ub, ue);
+                continue;
             }
-            // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
-            if (wave_count(__ballot(ok[0] && pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (ok[u]) {
-                        add(q[u].x);
-                        add(q[u].y);
-                        add(q[u].z);
-                        add(q[u].w);
+            // chunk v has no units left: flush what was stolen from it; pick the chunk with the most
+            // units left (a relaxed read of every claim counter; the claim itself decides)
+            __syncthreads();
+            if (v != c) {
+                for (uint32_t d = t; d < R; d += THREADS) {
+                    const uint32_t x = s_st[d];
+                    if (x) {
+                        atomicAdd(&a.steal[(uint64_t)d * nc + v], x);
+                        s_stot[d] += x;
+                        s_st[d] = 0;
                     }
                 }
-            } else {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (ok[u]) {
-                        add_run(q[u].x);
-                        add_run(q[u].y);
-                        add_run(q[u].z);
-                        add_run(q[u].w);
-                    }
+            }
+            if (t == 0) s_victim = 0xFFFFFFFFu;
+            __syncthreads();
+            uint32_t best = 0, bv = 0xFFFFFFFFu;
+            for (uint32_t x = t; x < nc; x += THREADS) {
+                const uint32_t cl = __hip_atomic_load(&a.claims[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t xu = units_of(x), xo = xu / 2;
+                const uint32_t left = xo + cl < xu ? xu - xo - cl : 0u;
+                if (left > best) {
+                    best = left;
+                    bv = x;
                 }
             }
+            // (any chunk with >= 2 units left: taking the last one from a busy owner gains nothing)
+            if (best >= 2) atomicMin(&s_victim, (0xFFFFu - min(best, 0xFFFFu)) << 16 | bv);
+            __syncthreads();
+            const uint32_t pick = s_victim;
+            if (pick == 0xFFFFFFFFu) break;
+            v = pick & 0xFFFFu;
+            if (t == 0) pend = atomicAdd(&a.claims[v], 1u);
         }
-        tail = beg + (uint64_t)nvec * 4;
     }
-    for (uint64_t i = tail + t; i < end; i += THREADS) add(a.keys[i]);
     __syncthreads();
-    // this chunk's digit counts: row sums plus the row's spill
+    // this chunk's digit counts: row sums plus the row's spill, minus the stolen keys' counts
     for (uint32_t d = t; d < R; d += THREADS) {
         uint32_t s = s_sp[d];
         for (uint32_t j = 0; j < R / 2; ++j) {
             const uint32_t x = s_j[d * RS + j];
             s += (x & 0xFFFFu) + (x >> 16);
         }
+        s -= s_stot[d];
         if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = s;
         else if (s) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], s);
     }
@@ -757,6 +843,24 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
             }
             a.table[(d0 + i) * R + c] = v;
             s += v;
+        }
+    } else if (a.steal != nullptr) {
+        // a work-stealing joint count: the stolen keys' counts join their chunks' rows, and the
+        // stealing state is cleared for the next joint count
+        if (blockIdx.x == 0)
+            for (uint32_t i = threadIdx.x; i < kJointBins; i += kScanThreads) a.claims[i] = 0u;
+#pragma unroll
+        for (int i = 0; i < kScanPerThread; ++i) {
+            if (base + i < a.m) {
+                const uint32_t x = a.steal[base + i];
+                uint32_t v = a.table[base + i];
+                if (x) {
+                    v += x;
+                    a.table[base + i] = v;
+                    a.steal[base + i] = 0u;
+                }
+                s += v;
+            }
         }
     } else {
 #pragma unroll
@@ -1691,18 +1795,6 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         // ... and, in slot 0, iff this lane's tile position is not before the chunk (head)
         const bool h0 = base >= head;
         head = 0;
-#ifdef RSORT_PRIO_ROT
-        // lab: several workgroups per CU (C2: 4) end in dispatch order (the older wins the CU's
-        // arbitration); rotating the wave priority per tile gives each the lead in turn
-        if constexpr (THREADS == 256) {
-            switch ((uint32_t)(((tb - cbeg) / T) + (c >> 8)) & 3u) {
-                case 0: __builtin_amdgcn_s_setprio(0); break;
-                case 1: __builtin_amdgcn_s_setprio(1); break;
-                case 2: __builtin_amdgcn_s_setprio(2); break;
-                default: __builtin_amdgcn_s_setprio(3); break;
-            }
-        }
-#endif
         // ---- 1. per-wave digit histogram (each wave clears its own counters first)
 #pragma unroll
         for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
@@ -1988,9 +2080,11 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
 // (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
 // the next tile's loads issued before the rank loop instead of after it, OPT & 4 keys and values
 // staged interleaved, OPT & 8 step 4 deferred to after the next tile's rank phase,
-// OPT & 16 / 32 the next tile's loads issued after step 2 / step 3 instead of after the rank phase)
+// OPT & 16 / 32 the next tile's loads issued after step 2 / step 3 instead of after the rank phase,
+// OPT & 64 keys and values through ONE staging array in turn: steps 3 and 4 for the keys, then for the
+// values at the same slots (kept in registers) -- half the LDS, so two workgroups fit per CU)
 template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
-__global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
+__global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;
@@ -2010,8 +2104,10 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
     // OPT & 4: one interleaved {key, value} array (8-B stores per pair) instead of two
     constexpr bool IL = (OPT & 4) != 0;
     constexpr bool DEFER = (OPT & 8) != 0;
+    constexpr bool SQ = (OPT & 64) != 0;
+    static_assert(!(SQ && (IL || DEFER)), "sequential staging: two plain arrays' worth of work in one");
     __shared__ __attribute__((aligned(16))) uint32_t s_k[IL ? 4 : CAP + 36];
-    __shared__ __attribute__((aligned(16))) uint32_t s_v[IL ? 4 : CAP + 36];
+    __shared__ __attribute__((aligned(16))) uint32_t s_v[(IL || SQ) ? 4 : CAP + 36];
     __shared__ __attribute__((aligned(16))) uint2 s_kv[IL ? CAP + 36 : 2];
     constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
     __shared__ uint32_t s_cnt[W * RS + 1];
@@ -2111,6 +2207,39 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     a.kout[gp + x] = kv[x];
                     a.vout[gp + x] = vv[x];
                 }
+        }
+    };
+
+    // SQ: one array's quad of whole line item / QPL from the staging array (the keys' or the values')
+    auto store_one = [&](uint32_t item, uint32_t *__restrict__ dst) {
+        const uint32_t V = item / QPL, q = (item % QPL) * 4u;
+        const uint2 lr = s_lrec[V];
+        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_k[(lr.y & 0xFFFFu) + q]);
+        const uint64_t gp = (uint64_t)(lr.x + q);
+        const uint32_t lo = lr.y >> 16;
+        if (lo <= q) {
+            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(dst + gp));
+        } else {
+#pragma unroll
+            for (uint32_t x = 0; x < 4; ++x)
+                if (lo <= q + x) dst[gp + x] = kv[x];
+        }
+    };
+    // SQ: one array's tails (from the staging array) into its carry registers, and its whole lines out
+    auto output_one = [&](const uint32_t S, const uint32_t wl, const uint32_t pending, const uint32_t nlines,
+                          uint32_t (&cr)[CPT], uint32_t *__restrict__ dst) {
+        const uint32_t tl0 = S + wl * G + sub * CPT;
+        const uint32_t ncarry = pending - wl * G;
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; i += 4) {
+            if (sub * CPT + i >= ncarry) break;
+            const u32x4 q4 = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+            cr[i] = q4.x; cr[i + 1] = q4.y; cr[i + 2] = q4.z; cr[i + 3] = q4.w;
+        }
+        const uint32_t nq = nlines * QPL;
+        for (uint32_t item = t; item < nq; item += 2 * THREADS) {
+            store_one(item, dst);
+            if (item + THREADS < nq) store_one(item + THREADS, dst);
         }
     };
 
@@ -2268,7 +2397,8 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                             u32x4{ck[i + 2], cv[i + 2], ck[i + 3], cv[i + 3]};
                     } else {
                         *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
-                        *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+                        if constexpr (!SQ)
+                            *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
                     }
                 }
             }
@@ -2297,6 +2427,7 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
             RS_STAMP(2);
             constexpr int SB = KPT < 8 ? KPT : 8;
             static_assert(KPT % SB == 0, "whole batches of slots");
+            uint32_t sidx[SQ ? KPT : 1];  // SQ: every slot's staging index, for the values after the keys
     #pragma unroll
             for (int j0 = 0; j0 < KPT; j0 += SB) {
                 uint32_t pp[SB];
@@ -2314,6 +2445,9 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                     if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
                     if constexpr (IL) {
                         s_kv[idx] = make_uint2(key[j], val[j]);
+                    } else if constexpr (SQ) {
+                        s_k[idx] = key[j];
+                        sidx[j] = idx;
                     } else {
                         s_k[idx] = key[j];
                         s_v[idx] = val[j];
@@ -2331,7 +2465,24 @@ __global__ __launch_bounds__(THREADS) void rs_scatter_pairs(ScatterArgs a) {
                 if (nb < cend) load_tile(nb, nkey, nval);
             }
 
-            if constexpr (DEFER) {
+            if constexpr (SQ) {
+                // the keys' lines and tails; then the values through the same slots: their carry into the
+                // segment heads, staged at the keys' indices, their lines and tails
+                output_one(S, wl, pending, nlines, ck, a.kout);
+                __syncthreads();
+                // (dword by dword: no barrier separates these from the staging below, so a whole quad
+                // past the carry's end could land after a staged value)
+    #pragma unroll
+                for (uint32_t i = 0; i < CPT; ++i)
+                    if (sub * CPT + i < carry) s_k[S + sub * CPT + i] = cv[i];
+    #pragma unroll
+                for (int j = 0; j < KPT; ++j) s_k[sidx[j]] = val[j];
+                __syncthreads();
+                output_one(S, wl, pending, nlines, cv, a.vout);
+                if (wl > 0) inv = 0;
+                carry = pending - wl * G;
+                g_run += cnt;
+            } else if constexpr (DEFER) {
                 pS = S;
                 pwl = wl;
                 ppend = pending;

@@ -107,7 +107,7 @@ def host_transport(group=None) -> "rs.HostTransport":
 
 def exchange_rounds(max_message: int, limit: int) -> tuple[int, int]:
     """(rounds, piece) for messages of up to max_message keys, <= limit keys each: the C planning
-    function rsort_multi_exchange_rounds (pieces a multiple of 64 keys, rounded down)."""
+    function rsort_multi_exchange_rounds (pieces a multiple of 64 keys, never above the limit)."""
     return rs.multi_exchange_rounds(max_message, limit)
 
 

@@ -22,6 +22,9 @@
 
 using namespace rsort;
 
+// the sequential-staging variant's own plan: 4096-pair tiles, 512 fixed chunks (two workgroups per CU)
+static ScatterArgs g_sb2;
+
 #define CK(x)                                                                     \
     do {                                                                          \
         hipError_t e_ = (x);                                                      \
@@ -53,6 +56,12 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&kb, n * 4));
     CK(hipMalloc(&vb, n * 4));
     CK(hipMalloc(&table, R * chunks * 4));
+    constexpr uint32_t TILE2 = 4096, CH2 = 512;
+    const uint64_t tiles2 = (n + TILE2 - 1) / TILE2, tpc2 = (tiles2 + CH2 - 1) / CH2;
+    const uint64_t chunk_keys2 = tpc2 * TILE2;
+    const uint32_t chunks2 = (uint32_t)((tiles2 + tpc2 - 1) / tpc2);
+    uint32_t *table2;
+    CK(hipMalloc(&table2, R * chunks2 * 4));
     CK(hipMalloc(&bsums, 4096));
     CK(hipMalloc(&stamps, chunks * 8 * 8));
     CK(hipMalloc(&cdf, (1u << 20) * 4));
@@ -71,7 +80,7 @@ int main(int argc, char **argv) {
     rs_gen_iota<<<65536, 256>>>(v0, n, 0);
     CK(hipDeviceSynchronize());
 
-    auto table_for = [&](const uint32_t *keys, uint32_t shift) {
+    auto table_for = [&](const uint32_t *keys, uint32_t shift, uint32_t *table, uint64_t chunk_keys, uint32_t chunks) {
         HistArgs h{};
         h.keys = keys;
         h.table = table;
@@ -107,14 +116,15 @@ int main(int argc, char **argv) {
     const uint32_t *in_k = k0, *in_v = v0;
     uint32_t shift = 0;
     if (pass == 1) {  // pass 0 first (64-B kernel), into ka/va; time pass 1 on it
-        table_for(k0, 0);
+        table_for(k0, 0, table, chunk_keys, chunks);
         rs_scatter_lines<8, 512, 16, kLineKeysPairs, true, kDigitShift, 2><<<chunks, 512>>>(args(k0, v0, ka, va, 0));
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(k0, ka, n * 4, hipMemcpyDeviceToDevice));
         CK(hipMemcpy(v0, va, n * 4, hipMemcpyDeviceToDevice));
         shift = 8;
     }
-    table_for(in_k, shift);
+    table_for(in_k, shift, table, chunk_keys, chunks);
+    table_for(in_k, shift, table2, chunk_keys2, chunks2);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -139,6 +149,11 @@ int main(int argc, char **argv) {
     // best round reported: clocks and thermals drift over a run) and checked against the first
     ScatterArgs sb = args(in_k, in_v, kb, vb, shift);
     sb.stamps = stamps;
+    g_sb2 = sb;
+    g_sb2.table = table2;
+    g_sb2.chunk_keys = chunk_keys2;
+    g_sb2.num_chunks = chunks2;
+    g_sb2.stamps = nullptr;
     struct Var {
         const char *name;
         void (*launch)(const ScatterArgs &, uint32_t);
@@ -152,6 +167,14 @@ int main(int argc, char **argv) {
              rs_scatter_pairs<8, 1024, 8><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 128-B 1024 x 8, CL", [](const ScatterArgs &x, uint32_t g) {
              rs_scatter_pairs<8, 1024, 8, 1><<<g, 1024>>>(x); }, 1e9f, {}},
+        {"rs_scatter_pairs 512 x 8 seq. staging, 512 ch", [](const ScatterArgs &x, uint32_t g) {
+             (void)x; (void)g;
+             rs_scatter_pairs<8, 512, 8, 0, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
+        {"rs_scatter_pairs 512 x 8 seq. staging CL", [](const ScatterArgs &x, uint32_t g) {
+             (void)x; (void)g;
+             rs_scatter_pairs<8, 512, 8, 1, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
+        {"rs_scatter_pairs 1024 x 8 seq. staging, 256 ch", [](const ScatterArgs &x, uint32_t g) {
+             rs_scatter_pairs<8, 1024, 8, 1, 1, 64><<<g, 1024>>>(x); }, 1e9f, {}},
     };
     const int rounds = env_int("PL_ROUNDS", 3);
     std::vector<uint32_t> refk(n), refv(n), gk(n), gv(n);

@@ -321,8 +321,9 @@ RSORT_API int rsort_multi_exchange_plan(int world, int me, int buckets, const in
                                         rsort_exchange_plan *out);
 
 /* 4. Exchange rounds. Messages of up to max_message keys (the plan's max_message), at most `limit`
- * keys each: *rounds equal pieces of *piece keys, a multiple of 64 keys rounded DOWN (never above
- * the limit; >= 64), rounds * piece >= max_message. (0, 0) for max_message 0. */
+ * keys each: *rounds equal pieces of *piece keys, a multiple of 64 keys (rounded up where that stays
+ * within the limit -- a message under the limit is one round -- else down: never above the limit;
+ * >= 64), rounds * piece >= max_message. (0, 0) for max_message 0. */
 RSORT_API int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, int64_t *rounds, int64_t *piece);
 
 /* ---------------------------------------------------------------- multi-GPU sort */
@@ -418,8 +419,8 @@ RSORT_API int rsort_multi_last_stats(rsort_multi_stats *out);
 RSORT_API int rsort_multi_inject_failure(int rank, int stage, int status);
 
 /* Largest message of one exchange round, in keys (default and maximum 2^28 = 1 GiB; >= 64).
- * Messages are cut into equal pieces of a multiple of 64 keys rounded DOWN, so no message exceeds
- * the limit even when it is not a multiple of 64. Process-wide; returns the previous value. Tests
+ * Messages are cut into equal pieces of a multiple of 64 keys, never above the limit, even when it
+ * is not a multiple of 64 (rsort_multi_exchange_rounds). Process-wide; returns the previous value. Tests
  * set small values to force several rounds. */
 RSORT_API int64_t rsort_set_exchange_piece(int64_t keys);
 

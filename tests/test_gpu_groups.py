@@ -440,8 +440,9 @@ for k, gen, n in ((3, uniform_keys, (1 << 21) + 3), (4, zipf_keys, (1 << 21) + 7
     d = rs.empty_u32(n)
     rs.sort_device(rs.from_numpy_u32(x), d, k, ws=ws, plan_=p)
     ok = np.array_equal(rs.to_numpy_u32(d), oracle_sort(x, k)) and rs.plan_check(p, ws) == 0
-    out.append(f"k{k}:{int(ok)}:{rs.plan_features(p)}:{rs.group_flags(p, ws) if k == 8 else ''}")
-print(" ".join(out))
+    flags = ",".join(map(str, rs.group_flags(p, ws))) if k == 8 else ""
+    out.append(f"k{k}:{int(ok)}:{rs.plan_features(p)}:{flags}")
+print("LAB " + " ".join(out))
 '''
 
 
@@ -462,7 +463,9 @@ def test_lab_switches_in_a_subprocess(env, feat4):
     r = subprocess.run([sys.executable, "-c", _LAB_SNIPPET, str(root / "cuda.radixsort_amd"), str(root / "tests")],
                        capture_output=True, text=True, timeout=240, env=e)
     assert r.returncode == 0, r.stderr[-2000:]
-    parts = r.stdout.split()
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("LAB ")]
+    assert line, r.stdout[-2000:]
+    parts = line[-1].split()[1:]
     assert [x.split(":")[1] for x in parts] == ["1", "1", "1"], r.stdout
     assert parts[0].split(":")[2] == str(feat4) and parts[1].split(":")[2] == str(feat4), r.stdout
-    assert parts[2].split(":")[3] == "[2, 2]", r.stdout  # Zipf keys: cut plans on passes 1 and 3
+    assert parts[2].split(":")[3] == "2,2", r.stdout  # Zipf keys: cut plans on passes 1 and 3

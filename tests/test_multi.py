@@ -163,12 +163,15 @@ def test_dist_sort_capacity_error_on_every_rank(tmp_path):
 
 
 def test_exchange_rounds_never_exceed_the_limit():
-    """pieces are a multiple of 64 keys rounded DOWN, so no message exceeds the limit
-    even when the limit is not a multiple of 64 (limit 65, max_message 130: pieces of 64, 3
-    rounds -- rounding up gave 128)."""
+    """pieces are a multiple of 64 keys, never above the limit, even when the limit is not
+    a multiple of 64 (limit 65, max_message 130: pieces of 64, 3 rounds -- rounding up gave 128); they
+    round up only where that stays within the limit, so a message under the limit is one round."""
     import multi
     assert multi.exchange_rounds(130, 65) == (3, 64)
     assert multi.exchange_rounds(0, 1 << 28) == (0, 0)
+    # a message that fits the limit is one round (C5's largest, ~2^27 keys: pieces rounded UP to 64)
+    assert multi.exchange_rounds(134107614, 1 << 28) == (1, 134107648)
+    assert multi.exchange_rounds(1 << 28, 1 << 28) == (1, 1 << 28)
     rng = np.random.default_rng(7)
     for _ in range(2000):
         m = int(rng.integers(1, 1 << 40))
