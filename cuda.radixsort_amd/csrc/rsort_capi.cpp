@@ -304,7 +304,12 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     a.split = 1;
     a.joint = joint;
     a.joint_enable = enable;
-    a.claims = claims;
+    // (RSORT_NO_STEAL=1 under RSORT_LAB=1: every workgroup counts its own chunk only -- A/B runs)
+    static const bool no_steal = [] {
+        const char *e = lab_env("RSORT_NO_STEAL");
+        return e != nullptr && e[0] == '1';
+    }();
+    a.claims = no_steal ? nullptr : claims;
     a.steal = steal;
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
     // the first joint count of a sort clears the counts and the work-stealing state (contiguous); a
