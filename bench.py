@@ -406,9 +406,7 @@ def self_launch(a) -> int:
     rank (a peer that died, a collective that never completes) ends the command instead of hanging it.
     This process never initialises HIP (it counts GPUs from the environment / device nodes) and never
     re-execs; the children inherit stdout, so rank 0's JSON line is this command's output."""
-    import signal
     import socket
-    import subprocess
     visible = visible_gpus()
     if os.environ.get("RSORT_BENCH_BACKEND", "") != "gloo" and visible < a.gpus:
         print(f"bench.py: --gpus {a.gpus} but {visible} GPU(s) visible (RSORT_BENCH_BACKEND=gloo rehearses "
@@ -423,14 +421,22 @@ def self_launch(a) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # (RCCL over dmabuf IPC on these hosts)
     limit = launch_timeout(a)
     env["RSORT_BENCH_TIMEOUT"] = str(int(limit))  # (the ranks bound their own collectives below it)
+    return run_group(cmd, env, limit, f"the {a.gpus} ranks")
+
+
+def run_group(cmd, env, limit, what, grace=10.0) -> int:
+    """Run cmd in a process group of its own and return its exit code; past `limit` seconds kill the
+    whole group (SIGTERM, then SIGKILL after `grace`) and return 124 with a message on stderr."""
+    import signal
+    import subprocess
     sys.stdout.flush()
     proc = subprocess.Popen(cmd, env=env, start_new_session=True)
     try:
         return proc.wait(timeout=limit)
     except subprocess.TimeoutExpired:
-        print(f"bench.py: the {a.gpus} ranks did not finish within {limit:.0f} s (a stalled or dead rank); "
+        print(f"bench.py: {what} did not finish within {limit:.0f} s (a stalled or dead rank); "
               f"killing process group {proc.pid}", file=sys.stderr, flush=True)
-        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+        for sig in (signal.SIGTERM, signal.SIGKILL):
             try:
                 os.killpg(proc.pid, sig)
             except ProcessLookupError:
@@ -440,6 +446,11 @@ def self_launch(a) -> int:
                 break
             except subprocess.TimeoutExpired:
                 continue
+        # (the group may outlive its leader: make sure nothing of it is left)
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
         return 124
     except BaseException:
         try:
