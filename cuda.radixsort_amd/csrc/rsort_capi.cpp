@@ -116,6 +116,14 @@ int k4_lines_lg() {
     return v;
 }
 
+bool k4_geom512() {
+    static const bool v = [] {
+        const char *e = lab_env("RSORT_K4_GEOM");
+        return e != nullptr && atoi(e) == 512;
+    }();
+    return v;
+}
+
 // Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
 // 16384-key tiles (rs_scatter_lines), pairs from 8192-key tiles; k <= 4 keys
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
@@ -133,6 +141,8 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:
     // 1.61 ms per pass against 1.75 ms with 4096-key tiles; at 2^26 0.120 against 0.113)
     if (k == 4 && !pairs && n >= ((int64_t)1 << k4_lines_lg())) return kGeomLines;
+    // (lab: RSORT_K4_GEOM=512 under RSORT_LAB runs k = 3, 4 keys on 512 x 16 line tiles)
+    if ((k == 3 || k == 4) && !pairs && k4_geom512() && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
     // lines: 2^26 keys, k = 4: 0.117 vs 0.144 ms per pass, dev/scatter_lab.hip); k <= 2 keeps
@@ -172,7 +182,8 @@ bool nx_tail() {
 // kernel (lane-ordered ranks, line-capable outputs: checked per sort) and a second table.
 bool next_plan(const rsort_plan &p) {
     const int g = geom_from_shape(p.threads, p.tile_keys, p.pairs);
-    return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 && (g == kGeomSmall || g == kGeomLines);
+    return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 &&
+           (g == kGeomSmall || g == kGeomLines || g == kGeomK4);
 }
 
 int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int partition = 0) {

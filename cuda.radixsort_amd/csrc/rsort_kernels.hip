@@ -2809,6 +2809,12 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         }
     }
     if constexpr (BITS <= 4 && !PAIRS) {
+        if constexpr (BITS >= 3) {
+            // k = 3, 4 keys on 512 x 16 line tiles (RSORT_K4_GEOM=512 under RSORT_LAB: A/B of two
+            // 8192-key workgroups per CU against four 4096-key ones)
+            constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
+            if (geom == kGeomK4 && rank == kRankAtomic && aligned16) return reg_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, 3>();
+        }
         if (geom == kGeomK4) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomK4>(rank);
     }
     return nullptr;
@@ -3000,6 +3006,12 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomSmall &&
         rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
         constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
+        fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
+                       : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
+    }
+    if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomK4 &&
+        rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
+        constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
         fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
                        : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
     }
