@@ -116,14 +116,6 @@ int k4_lines_lg() {
     return v;
 }
 
-bool k4_geom512() {
-    static const bool v = [] {
-        const char *e = lab_env("RSORT_K4_GEOM");
-        return e != nullptr && atoi(e) == 512;
-    }();
-    return v;
-}
-
 // Tile geometry for one sort: for k = 5..8, keys-only sorts write whole 64-B lines from
 // 16384-key tiles (rs_scatter_lines), pairs from 8192-key tiles; k <= 4 keys
 // use 8192-key tiles; everything else 4096-key tiles -- as do inputs too small to give every
@@ -141,8 +133,6 @@ int choose_geom(int64_t n, int k, int pairs, int rank, int partition, int cus) {
     // k = 4 keys from 2^28 on: the same 1024-thread line tiles (dev/scatter_lab LAB_K4 at 2^30:
     // 1.61 ms per pass against 1.75 ms with 4096-key tiles; at 2^26 0.120 against 0.113)
     if (k == 4 && !pairs && n >= ((int64_t)1 << k4_lines_lg())) return kGeomLines;
-    // (lab: RSORT_K4_GEOM=512 under RSORT_LAB runs k = 3, 4 keys on 512 x 16 line tiles)
-    if ((k == 3 || k == 4) && !pairs && k4_geom512() && n >= enough * geom_tile_keys(kGeomK4)) return kGeomK4;
     if (k >= 5 && k <= 8 && pairs && n >= enough * geom_tile_keys(kGeomLinesPairs)) return kGeomLinesPairs;
     // k = 3, 4 keys run 4096-key tiles through rs_scatter_lines (kGeomSmall's shape; whole 128-B
     // lines: 2^26 keys, k = 4: 0.117 vs 0.144 ms per pass, dev/scatter_lab.hip); k <= 2 keeps
@@ -182,8 +172,7 @@ bool nx_tail() {
 // kernel (lane-ordered ranks, line-capable outputs: checked per sort) and a second table.
 bool next_plan(const rsort_plan &p) {
     const int g = geom_from_shape(p.threads, p.tile_keys, p.pairs);
-    return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 &&
-           (g == kGeomSmall || g == kGeomLines || g == kGeomK4);
+    return (p.k_bits == 3 || p.k_bits == 4) && !p.pairs && p.passes >= 2 && (g == kGeomSmall || g == kGeomLines);
 }
 
 int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int partition = 0) {
@@ -225,8 +214,6 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
     if (joint_plan(*p)) {
         ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
-        ws += align256((size_t)kJointBins * 4);               // work-stealing claims (joint counts)
-        ws += align256((size_t)p->table_entries * 4);         // ... and the stolen keys' digit counts
         ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
         ws += align256((size_t)kPlanWords * 4);               // cut plan
         ws += align256((size_t)kPieceSlots * kJointBins * 4); // its piece counts
@@ -251,8 +238,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 }
 
 struct Carve {
-    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *claims, *steal, *bounds, *plan, *pcounts, *table2, *done,
-        *table3;
+    uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done, *table3;
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -273,10 +259,6 @@ Carve carve(const rsort_plan &p, void *ws) {
     if (joint_plan(p)) {
         c.joint = (uint32_t *)q;
         q += align256((size_t)kJointBins * kJointBins * 4);
-        c.claims = (uint32_t *)q;  // (claims and steal follow the joint counts: one memset clears all three)
-        q += align256((size_t)kJointBins * 4);
-        c.steal = (uint32_t *)q;
-        q += align256((size_t)p.table_entries * 4);
         c.bounds = (uint32_t *)q;
         q += align256((size_t)2 * kBoundsWords * 4);
         c.plan = (uint32_t *)q;
@@ -303,7 +285,7 @@ Carve carve(const rsort_plan &p, void *ws) {
 // adds runs of equal pairs once (rs_histogram's run path), so pass 3 gets its own cut plan too.
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                        uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
-                       uint32_t *pcounts, hipStream_t s, bool zero_joint, uint32_t *claims, uint32_t *steal) {
+                       uint32_t *pcounts, hipStream_t s, bool zero_joint) {
     HistArgs a{};
     a.keys = keys;
     a.table = table;
@@ -315,19 +297,10 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     a.split = 1;
     a.joint = joint;
     a.joint_enable = enable;
-    // (RSORT_NO_STEAL=1 under RSORT_LAB=1: every workgroup counts its own chunk only -- A/B runs)
-    static const bool no_steal = [] {
-        const char *e = lab_env("RSORT_NO_STEAL");
-        return e != nullptr && e[0] == '1';
-    }();
-    a.claims = no_steal ? nullptr : claims;
-    a.steal = steal;
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
-    // the first joint count of a sort clears the counts and the work-stealing state (contiguous); a
-    // later one finds them cleared by the copy-mode histogram / the scan that used them (or, where that
-    // pass fell back, is disabled by `enable`)
-    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)((char *)steal - (char *)joint) + (size_t)p.table_entries * 4, s) !=
-                          hipSuccess)
+    // the first joint count of a sort clears the counts; a later one finds them cleared by the
+    // copy-mode histogram that used them (or, where that pass fell back, is disabled by `enable`)
+    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess)
         return RSORT_ERR_HIP;
     if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
     // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
@@ -381,15 +354,9 @@ int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t 
 }
 
 int do_scan(const rsort_plan &p, uint32_t *table, uint32_t *bsums, hipStream_t s, uint32_t *zero = nullptr,
-            uint32_t *done = nullptr, const Carve *cut = nullptr, const uint32_t *group_flag = nullptr,
-            const Carve *stolen = nullptr) {
+            uint32_t *done = nullptr, const Carve *cut = nullptr, const uint32_t *group_flag = nullptr) {
     ScanArgs a{};
     a.done = done;
-    if (stolen != nullptr) {
-        // after a work-stealing joint count: its stolen counts join the table
-        a.steal = stolen->steal;
-        a.claims = stolen->claims;
-    }
     if (cut != nullptr) {
         // a digit-group pass: under a cut plan the scan assembles the table first
         a.group_flag = group_flag;
@@ -515,8 +482,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         if (count_joint) {
             const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
             if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
-                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0, c.claims,
-                                         c.steal)))
+                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0)))
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
@@ -527,8 +493,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // raw tables: no scan at all, the histogram cleared the next table), every later table by the
         // previous scatter's last workgroup (raw tables: by every workgroup of the pass itself)
         if (!(nextc && i > 0) && !rawt &&
-            (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds,
-                          count_joint ? &c : nullptr)))
+            (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds)))
             return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
         // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the

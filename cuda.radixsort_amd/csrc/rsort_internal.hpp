@@ -89,14 +89,7 @@ struct HistArgs {
     uint32_t *zero;
     uint64_t zero_n;
     uint32_t *done;
-    // joint counts with work stealing (rs_histogram JOINT, split 1): claims[kJointBins] (zero on entry)
-    // counts the claimed units of each chunk's second half, steal[R x C] (zero on entry) receives the
-    // digit counts of the keys other workgroups counted for a chunk; rs_scan_reduce adds them into
-    // the table and clears both (ScanArgs::steal)
-    uint32_t *claims;
-    uint32_t *steal;
 };
-constexpr uint64_t kStealUnit = 65536;  // keys per claimed unit of a joint count
 
 struct ScatterArgs {
     const uint32_t *kin;
@@ -155,9 +148,6 @@ struct ScanArgs {
     uint32_t *joint;
     const uint32_t *plan;
     const uint32_t *pcounts;
-    // after a work-stealing joint count (HistArgs::steal): table += steal, then steal and claims cleared
-    uint32_t *steal;
-    uint32_t *claims;
 };
 
 // Launchers (rsort_kernels.hip). All return hipSuccess or the launch error.

@@ -428,19 +428,13 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     constexpr uint32_t RS = R / 2 + 1;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t *s_sp = s_j + R * RS;
-    // work stealing (a.claims): stolen keys' digit counts, per victim (s_st) and in total (s_stot)
-    __shared__ uint32_t s_st[R], s_stot[R];
-    __shared__ uint32_t s_claim, s_victim;
     const uint32_t t = threadIdx.x;
     RS_WG_T0
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
-    for (uint32_t i = t; i < R; i += THREADS) s_st[i] = s_stot[i] = 0;
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
     // add inc (<= 64) to the 16-bit counter of pair (d, e); the add that takes it to 2^15 moves 2^15
-    // to the row's spill word and to the global count (the counter stays below 2^15 + 64). Keys of a
-    // stolen unit also count their digit in s_st (they are not this chunk's).
-    bool stolen = false;
+    // to the row's spill word and to the global count (the counter stays below 2^15 + 64)
     auto add_pair = [&](uint32_t d, uint32_t e, uint32_t inc) {
         const uint32_t wi = d * RS + (e >> 1), sh = (e & 1u) << 4;
         const uint32_t before = (atomicAdd(&s_j[wi], inc << sh) >> sh) & 0xFFFFu;
@@ -449,7 +443,6 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             atomicAdd(&s_sp[d], 0x8000u);
             atomicAdd(&a.joint[e * R + d], 0x8000u);
         }
-        if (stolen) atomicAdd(&s_st[d], inc);
     };
     auto add = [&](uint32_t x) { add_pair((x >> s0) & (R - 1u), (x >> s1) & (R - 1u), 1u); };
     // Clustered input (runs of equal keys: sorted or duplicate-heavy data, and every pass after a cut
@@ -472,138 +465,59 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             add_pair(pr & 0xFFu, pr >> 8, end - lane_id());
         }
     };
-    // keys [beg, end) (beg 16-B aligned when a.vec) into the joint counts
-    auto count_keys = [&](uint64_t beg, uint64_t end) {
-        uint64_t tail = beg;
-        if (a.vec) {
-            const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
-            const uint32_t nvec = (uint32_t)((end - beg) / 4);
-            constexpr int U = 4;
-            for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
-                u32x4 q[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t v = v0 + u * THREADS;
-                    ok[u] = v < nvec;
-                    q[u] = ok[u] ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
-                }
-                // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
-                if (wave_count(__ballot(ok[0] && pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        if (ok[u]) {
-                            add(q[u].x);
-                            add(q[u].y);
-                            add(q[u].z);
-                            add(q[u].w);
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        if (ok[u]) {
-                            add_run(q[u].x);
-                            add_run(q[u].y);
-                            add_run(q[u].z);
-                            add_run(q[u].w);
-                        }
-                    }
-                }
-            }
-            tail = beg + (uint64_t)nvec * 4;
-        }
-        for (uint64_t i = tail + t; i < end; i += THREADS) add(a.keys[i]);
-    };
     const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
     const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
     const uint64_t beg = min(cbeg + sub * part, cend);
     const uint64_t end = min(beg + part, cend);
-    if (a.claims == nullptr || S != 1) {
-        count_keys(beg, end);
-    } else {
-        // Work stealing (the counts do not depend on which workgroup adds them; round 5): a chunk is
-        // units of kStealUnit keys; its first half is its own workgroup's, the second half goes to
-        // whoever claims it first (a.claims[chunk], one global add per unit, issued a unit ahead). A
-        // workgroup done with its chunk claims units of the chunks with the most units left. Stolen
-        // keys' digit counts go to a.steal[d][chunk] (added into the table by the scan) and are taken
-        // out of this chunk's row sums; the joint counts are global anyway. Skewed (clustered) passes
-        // end with their slowest chunks instead of waiting for them (Zipf pass 2: 271 vs ~240 us/Mkey).
-        const uint32_t nc = a.num_chunks;
-        auto units_of = [&](uint32_t v) {
-            const uint64_t vb = (uint64_t)v * a.chunk_keys, ve = min(vb + a.chunk_keys, a.n);
-            return (uint32_t)(ve > vb ? (ve - vb + kStealUnit - 1) / kStealUnit : 0);
-        };
-        auto unit_range = [&](uint32_t v, uint32_t u, uint64_t &ub, uint64_t &ue) {
-            const uint64_t vb = (uint64_t)v * a.chunk_keys, ve = min(vb + a.chunk_keys, a.n);
-            ub = min(vb + (uint64_t)u * kStealUnit, ve);
-            ue = min(ub + kStealUnit, ve);
-        };
-        const uint32_t nu = units_of(c), own = nu / 2;
-        // the first half: no claims
-        count_keys(cbeg, min(cbeg + (uint64_t)own * kStealUnit, cend));
-        // the second half and then the other chunks' second halves: claim unit by unit (the next
-        // claim's global add is issued before the current unit is counted)
-        uint32_t v = c;
-        uint32_t pend = 0u;  // thread 0: the claim in flight for chunk v
-        if (t == 0) pend = atomicAdd(&a.claims[v], 1u);
-        for (;;) {
-            __syncthreads();  // (s_claim / s_victim reuse)
-            if (t == 0) s_claim = pend;
-            __syncthreads();
-            const uint32_t u = s_claim, vu = units_of(v), vo = vu / 2;
-            if (vo + u < vu) {
-                if (t == 0) pend = atomicAdd(&a.claims[v], 1u);  // the next one, in flight
-                uint64_t ub, ue;
-                unit_range(v, vo + u, ub, ue);
-                stolen = v != c;
-                count_keys(ub, ue);
-                continue;
+    uint64_t tail = beg;
+    if (a.vec) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + beg);
+        const uint32_t nvec = (uint32_t)((end - beg) / 4);
+        constexpr int U = 4;
+        for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
+            u32x4 q[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = v0 + u * THREADS;
+                ok[u] = v < nvec;
+                q[u] = ok[u] ? __builtin_nontemporal_load(p + v) : u32x4{0, 0, 0, 0};
             }
-            // chunk v has no units left: flush what was stolen from it; pick the chunk with the most
-            // units left (a relaxed read of every claim counter; the claim itself decides)
-            __syncthreads();
-            if (v != c) {
-                for (uint32_t d = t; d < R; d += THREADS) {
-                    const uint32_t x = s_st[d];
-                    if (x) {
-                        atomicAdd(&a.steal[(uint64_t)d * nc + v], x);
-                        s_stot[d] += x;
-                        s_st[d] = 0;
+            // one clustering test per batch: >= 8 lanes whose first quad starts and ends with one pair
+            if (wave_count(__ballot(ok[0] && pair_of(q[0].x) == pair_of(q[0].w))) < 8) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (ok[u]) {
+                        add(q[u].x);
+                        add(q[u].y);
+                        add(q[u].z);
+                        add(q[u].w);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (ok[u]) {
+                        add_run(q[u].x);
+                        add_run(q[u].y);
+                        add_run(q[u].z);
+                        add_run(q[u].w);
                     }
                 }
             }
-            if (t == 0) s_victim = 0xFFFFFFFFu;
-            __syncthreads();
-            uint32_t best = 0, bv = 0xFFFFFFFFu;
-            for (uint32_t x = t; x < nc; x += THREADS) {
-                const uint32_t cl = __hip_atomic_load(&a.claims[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t xu = units_of(x), xo = xu / 2;
-                const uint32_t left = xo + cl < xu ? xu - xo - cl : 0u;
-                if (left > best) {
-                    best = left;
-                    bv = x;
-                }
-            }
-            // (any chunk with >= 2 units left: taking the last one from a busy owner gains nothing)
-            if (best >= 2) atomicMin(&s_victim, (0xFFFFu - min(best, 0xFFFFu)) << 16 | bv);
-            __syncthreads();
-            const uint32_t pick = s_victim;
-            if (pick == 0xFFFFFFFFu) break;
-            v = pick & 0xFFFFu;
-            if (t == 0) pend = atomicAdd(&a.claims[v], 1u);
         }
+        tail = beg + (uint64_t)nvec * 4;
     }
+    for (uint64_t i = tail + t; i < end; i += THREADS) add(a.keys[i]);
     __syncthreads();
-    // this chunk's digit counts: row sums plus the row's spill, minus the stolen keys' counts
+    // this chunk's digit counts: row sums plus the row's spill
     for (uint32_t d = t; d < R; d += THREADS) {
         uint32_t s = s_sp[d];
         for (uint32_t j = 0; j < R / 2; ++j) {
             const uint32_t x = s_j[d * RS + j];
             s += (x & 0xFFFFu) + (x >> 16);
         }
-        s -= s_stot[d];
         if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = s;
         else if (s) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], s);
     }
@@ -843,24 +757,6 @@ __global__ __launch_bounds__(kScanThreads) void rs_scan_reduce(ScanArgs a) {
             }
             a.table[(d0 + i) * R + c] = v;
             s += v;
-        }
-    } else if (a.steal != nullptr) {
-        // a work-stealing joint count: the stolen keys' counts join their chunks' rows, and the
-        // stealing state is cleared for the next joint count
-        if (blockIdx.x == 0)
-            for (uint32_t i = threadIdx.x; i < kJointBins; i += kScanThreads) a.claims[i] = 0u;
-#pragma unroll
-        for (int i = 0; i < kScanPerThread; ++i) {
-            if (base + i < a.m) {
-                const uint32_t x = a.steal[base + i];
-                uint32_t v = a.table[base + i];
-                if (x) {
-                    v += x;
-                    a.table[base + i] = v;
-                    a.steal[base + i] = 0u;
-                }
-                s += v;
-            }
         }
     } else {
 #pragma unroll
@@ -2809,12 +2705,6 @@ static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
         }
     }
     if constexpr (BITS <= 4 && !PAIRS) {
-        if constexpr (BITS >= 3) {
-            // k = 3, 4 keys on 512 x 16 line tiles (RSORT_K4_GEOM=512 under RSORT_LAB: A/B of two
-            // 8192-key workgroups per CU against four 4096-key ones)
-            constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
-            if (geom == kGeomK4 && rank == kRankAtomic && aligned16) return reg_lines<BITS, TH, KP, kLineKeys, false, kDigitShift, 3>();
-        }
         if (geom == kGeomK4) return scatter_cf<BITS, PAIRS, kDigitShift, kGeomK4>(rank);
     }
     return nullptr;
@@ -3006,12 +2896,6 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
     if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomSmall &&
         rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
         constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
-        fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
-                       : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
-    }
-    if (a.n <= ((uint64_t)1 << 26) && !pairs && dmode == kDigitShift && geom == kGeomK4 &&
-        rank_algo == kRankAtomic && aligned16 && (bits == 3 || bits == 4)) {
-        constexpr int TH = kGeomShape[kGeomK4].threads, KP = kGeomShape[kGeomK4].kpt;
         fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
                        : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
     }
