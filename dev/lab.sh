@@ -224,6 +224,26 @@ sqpmc)
     done
     python3 dev/sqpmc.py gpurun_out
     ;;
+sqc2)
+    # SQ counters of the C2 sort (bench.py --keys 2^26 --k 4), three passes of <= 8 counters, against a C3
+    # sort (2^29 keys, k = 8): is the k = 4 pass LDS-bound? (dev/sqpmc.py)
+    P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM"
+    P2="SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS"
+    P3="SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS SQ_BUSY_CYCLES"
+    i=0
+    for P in "$P1" "$P2" "$P3"; do
+        i=$((i + 1))
+        for cfg in "c2:--keys 67108864 --k 4" "keys:--keys 536870912"; do
+            tag=${cfg%%:*}
+            rm -rf "$R/gpurun_out/sqpmc_${tag}_$i"
+            (cd /tmp && TMPDIR=/tmp timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$R/gpurun_out/sqpmc_${tag}_$i" -- \
+                python3 "$R/bench.py" ${cfg#*:} --steps 1 --warmup 1 --no-cpu --no-e2e --no-vendor --configs "" \
+                > "$R/gpurun_out/sqpmc_${tag}_$i.log" 2>&1)
+            stop_unless_ok $? "sqc2 $tag $i"
+        done
+    done
+    python3 dev/sqpmc.py gpurun_out c2,keys
+    ;;
 sqzipf)
     # SQ counters per dispatch of the Zipf-keys passes (bench.py --dist zipf, 2^29 keys), in issue order:
     # LDS address / bank conflicts of the clustered passes against the first (dev/sqpmc.py --order)

@@ -23,7 +23,7 @@ if len(sys.argv) > 3 and sys.argv[2] == "--order":
         names = names or sorted(cs)
         print(did, kn.split("(")[0].replace("void rsort::", "")[-12:], " ".join(f"{c[3:]}={cs[c]:.3g}" for c in names))
     sys.exit(0)
-for prog in ("pairs", "keys"):
+for prog in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("pairs", "keys")):
     agg = defaultdict(lambda: defaultdict(list))
     for d in sorted(root.glob(f"sqpmc_{prog}_*")):
         if not d.is_dir():
