@@ -1402,7 +1402,9 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
 // below d) + (keys of digit d in chunks before c) from the whole table (R x C words: 64 KB at C2,
 // held in each XCD's L2 after the first reads) instead of one workgroup scanning it at the end of the
 // previous pass (tail_scan: ~5 us on the critical path of every pass). TPR = THREADS / R threads per
-// row, each summing every TPR-th quad of it. Returns false (in every thread) when the table does not
+// row, each summing every TPR-th quad of it, 8 quads in flight; the caller issues its first tile's
+// loads before (C2: 0.1183 vs 0.1206 ms per pass against one quad at a time behind no loads,
+// dev/lab.sh ab). Returns false (in every thread) when the table does not
 // hold exactly n keys: the caller then writes nothing (no offset can leave the output), and workgroup
 // 0 records it for rsort_plan_check. All threads must call it; ends with a barrier.
 template <int THREADS, uint32_t R>
@@ -1416,11 +1418,22 @@ __device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint6
     uint32_t all = 0, below = 0;
     if ((C & 3u) == 0u) {  // (rows start 16-B aligned: the table is)
         const u32x4 *r4 = reinterpret_cast<const u32x4 *>(row);
-        for (uint32_t q = sub; q < C / 4u; q += TPR) {
-            const u32x4 v = r4[q];
-            const uint32_t c0 = q * 4u;
-            all += v.x + v.y + v.z + v.w;
-            below += (c0 < c ? v.x : 0u) + (c0 + 1u < c ? v.y : 0u) + (c0 + 2u < c ? v.z : 0u) + (c0 + 3u < c ? v.w : 0u);
+        const uint32_t nq = C / 4u;
+        constexpr uint32_t RB = 8;  // quads in flight per thread
+        for (uint32_t q0 = sub; q0 < nq; q0 += RB * TPR) {
+            u32x4 v[RB];
+#pragma unroll
+            for (uint32_t i = 0; i < RB; ++i) {
+                const uint32_t q = q0 + i * TPR;
+                v[i] = q < nq ? r4[q] : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < RB; ++i) {
+                const uint32_t c0 = (q0 + i * TPR) * 4u;
+                all += v[i].x + v[i].y + v[i].z + v[i].w;
+                below += (c0 < c ? v[i].x : 0u) + (c0 + 1u < c ? v[i].y : 0u) + (c0 + 2u < c ? v[i].z : 0u) +
+                         (c0 + 3u < c ? v[i].w : 0u);
+            }
         }
     } else {
         for (uint32_t x = sub; x < C; x += TPR) {
@@ -1552,6 +1565,33 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     const bool leader = sub == 0;
     const uint32_t glead = lane & ~(TPD - 1u);
     uint32_t g_run = 0, carry = 0, inv = 0;
+    const uint32_t base = w * SEG + lane;
+    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        uint32_t lb = base;  // opaque: one lane offset + immediate slot offsets, nothing hoisted
+        asm volatile("" : "+v"(lb));
+        const uint32_t *__restrict__ tk = a.kin + tb + lb;
+        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb + lb : nullptr;
+        if (valid == T) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                // NT & 1: non-temporal key/value loads (dev/scatter_lab experiment)
+                k[j] = (NT & 1) ? __builtin_nontemporal_load(tk + j * kWave) : tk[j * kWave];
+                if constexpr (PAIRS) v[j] = (NT & 1) ? __builtin_nontemporal_load(tv + j * kWave) : tv[j * kWave];
+            }
+        } else {
+            const uint32_t lim = valid > lb ? valid - lb : 0u;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool in = (uint32_t)(j * kWave) < lim;
+                k[j] = in ? tk[j * kWave] : 0u;
+                if constexpr (PAIRS) v[j] = in ? tv[j * kWave] : 0u;
+            }
+        }
+    };
+    uint32_t key[KPT];
+    uint32_t val[PAIRS ? KPT : 1];
+    if (cbeg < cend) load_tile(cbeg, key, val);
     if constexpr (NX) {
         // this workgroup's share of the table the pass after next counts into (nobody reads that
         // one in this pass) is cleared on the way
@@ -1597,30 +1637,6 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         atomicAdd(&s_next[((d * 2 + slot) * R + e) * NXR + (lane & (NXR - 1))], 1u);
     };
 
-    const uint32_t base = w * SEG + lane;
-    auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
-        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-        uint32_t lb = base;  // opaque: one lane offset + immediate slot offsets, nothing hoisted
-        asm volatile("" : "+v"(lb));
-        const uint32_t *__restrict__ tk = a.kin + tb + lb;
-        const uint32_t *__restrict__ tv = PAIRS ? a.vin + tb + lb : nullptr;
-        if (valid == T) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                // NT & 1: non-temporal key/value loads (dev/scatter_lab experiment)
-                k[j] = (NT & 1) ? __builtin_nontemporal_load(tk + j * kWave) : tk[j * kWave];
-                if constexpr (PAIRS) v[j] = (NT & 1) ? __builtin_nontemporal_load(tv + j * kWave) : tv[j * kWave];
-            }
-        } else {
-            const uint32_t lim = valid > lb ? valid - lb : 0u;
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const bool in = (uint32_t)(j * kWave) < lim;
-                k[j] = in ? tk[j * kWave] : 0u;
-                if constexpr (PAIRS) v[j] = in ? tv[j * kWave] : 0u;
-            }
-        }
-    };
 
     // one 16-B quad of line L at quad offset q -> global; every key of an LDS line has the line's
     // digit, which locates the line's segment record (info)
@@ -1677,9 +1693,6 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         if (two) store_quad(L1, q1, kv1, vv1, in1, d1);
     };
 
-    uint32_t key[KPT];
-    uint32_t val[PAIRS ? KPT : 1];
-    if (cbeg < cend) load_tile(cbeg, key, val);
     uint32_t hotd = 0xFFFFFFFFu;  // CL: the wave's last aggregated digit (none yet)
 
     for (uint64_t tb = cbeg; tb < cend; tb += T) {
