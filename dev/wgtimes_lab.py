@@ -28,6 +28,8 @@ ap.add_argument("--hist", action="store_true",
                 help="also the joint-count histograms (passes 0 and 2) and what the slowest pass-2 chunks hold")
 ap.add_argument("--reps", type=int, default=0,
                 help="rate correlation over this many more sorts: by XCC, by physical CU, by chunk (VERDICT r4 #3)")
+ap.add_argument("--hxcc", type=int, default=0,
+                help="the joint-count histograms' workgroup durations by XCC over this many sorts (then exit)")
 a = ap.parse_args()
 n = 1 << a.log2n
 lib = rs._lib()
@@ -152,6 +154,30 @@ def eta2(y, g):
     return float(b / tot)
 
 
+def hist_xcc(reps):
+    """The joint-count histograms (passes 0, 2; one chunk per workgroup, a pure read of the keys): their
+    workgroups' durations by XCC (the lab build packs XCC_ID over the range's end word, as for the
+    scatter), and the wall against the mean -- does the pass wait for one half of the XCCs?"""
+    for r in range(reps):
+        rs.sort_device(keys, out, a.k, vals_in=vals, vals_out=vout, ws=ws, plan_=p)
+        torch.cuda.synchronize()
+        both = np.zeros(8 * 2048 * 4 + 4 * 256 * 4, dtype=np.uint64)
+        assert fn(both.ctypes.data) == 0
+        hb = both[8 * 2048 * 4:].reshape(4, 256, 4)
+        for ps in (0, 2):
+            t0, t1 = hb[ps, :, 0].astype(np.int64), hb[ps, :, 1].astype(np.int64)
+            xcc = (hb[ps, :, 3] >> np.uint64(32)).astype(np.int64) & 15
+            dur = (t1 - t0) * 10 / 1e3
+            wall = (t1.max() - t0.min()) * 10 / 1e3
+            by = [dur[xcc == x].mean() if (xcc == x).any() else float("nan") for x in range(8)]
+            print(f"sort {r} joint histogram pass {ps}: wall {wall:7.1f} us, dur min/med/max {dur.min():6.1f} "
+                  f"{np.median(dur):6.1f} {dur.max():6.1f}, start spread {(t0.max() - t0.min()) * 10 / 1e3:5.1f}, "
+                  f"by XCC " + " ".join(f"{v:6.1f}" for v in by))
+
+
+if a.hxcc:
+    hist_xcc(a.hxcc)
+    sys.exit(0)
 buf, hbuf, where = records()
 print("modes", rs.group_flags(p, ws), "chunks", p.num_chunks)
 for ps in range(p.passes):
