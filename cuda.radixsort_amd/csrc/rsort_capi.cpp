@@ -157,6 +157,16 @@ bool cut_weights() {
     return v;
 }
 
+// RSORT_PIECE_ROWS=0 under RSORT_LAB=1: cut plans count all their pieces from the keys (no per-chunk
+// joint-count rows; the round-4 scheme) for A/B runs
+bool piece_rows() {
+    static const bool v = [] {
+        const char *e = lab_env("RSORT_PIECE_ROWS");
+        return !(e != nullptr && e[0] == '0');
+    }();
+    return v;
+}
+
 // RSORT_NX_TAIL=1 under RSORT_LAB=1: next-digit plans scan each pass's table in its last workgroup
 // (the round-3 scheme) instead of every workgroup of the next pass summing the raw counts (A/B runs)
 bool nx_tail() {
@@ -213,10 +223,11 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     ws += align256((size_t)p->scan_blocks * 4);              // scan block sums
     ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
     if (joint_plan(*p)) {
-        ws += align256((size_t)kJointBins * kJointBins * 4);  // joint counts [next digit][digit]
-        ws += align256((size_t)2 * kBoundsWords * 4);         // group bounds of passes 1 and 3
-        ws += align256((size_t)kPlanWords * 4);               // cut plan
-        ws += align256((size_t)kPieceSlots * kJointBins * 4); // its piece counts
+        ws += align256((size_t)kJointBins * kJointBins * 4 + 4);  // joint counts [next digit][digit], rows counter
+        ws += align256((size_t)2 * kBoundsWords * 4);             // group bounds of passes 1 and 3
+        ws += align256((size_t)kPlanWords * 4);                   // cut plan
+        ws += align256((size_t)kPieceSlots * kJointBins * 4);     // its piece counts
+        ws += align256((size_t)kRowsWords * 4);                   // per-chunk joint-count rows (64 MiB)
     }
     if (!partition && next_plan(*p)) {
         ws += align256((size_t)p->table_entries * 4);  // the next pass's table
@@ -239,6 +250,7 @@ int partition_bits(int64_t n, int num_buckets, int pairs) {
 
 struct Carve {
     uint32_t *tmp_k, *tmp_v, *table, *bsums, *starts, *joint, *bounds, *plan, *pcounts, *table2, *done, *table3;
+    uint32_t *rows, *rows_cnt;  // joint plans: per-chunk joint-count rows (HistArgs::rows), their counter
 };
 
 Carve carve(const rsort_plan &p, void *ws) {
@@ -258,13 +270,16 @@ Carve carve(const rsort_plan &p, void *ws) {
     q += align256((size_t)(p.bins + 1) * 4);
     if (joint_plan(p)) {
         c.joint = (uint32_t *)q;
-        q += align256((size_t)kJointBins * kJointBins * 4);
+        c.rows_cnt = c.joint + kJointBins * kJointBins;  // (cleared with the joint counts)
+        q += align256((size_t)kJointBins * kJointBins * 4 + 4);
         c.bounds = (uint32_t *)q;
         q += align256((size_t)2 * kBoundsWords * 4);
         c.plan = (uint32_t *)q;
         q += align256((size_t)kPlanWords * 4);
         c.pcounts = (uint32_t *)q;
         q += align256((size_t)kPieceSlots * kJointBins * 4);
+        c.rows = (uint32_t *)q;
+        q += align256((size_t)kRowsWords * 4);
     }
     if (next_plan(p)) {
         c.table2 = (uint32_t *)q;
@@ -284,9 +299,11 @@ Carve carve(const rsort_plan &p, void *ws) {
 // cut plan's scan), not after fixed chunks. After a cut plan the input is clustered: the joint count
 // adds runs of equal pairs once (rs_histogram's run path), so pass 3 gets its own cut plan too.
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
-                       uint32_t *joint, const uint32_t *enable, uint32_t *bounds, uint32_t *plan,
-                       uint32_t *pcounts, hipStream_t s, bool zero_joint) {
+                       uint32_t *joint, const uint32_t *enable, hipStream_t s, bool zero_joint,
+                       uint32_t *rows, uint32_t *rows_cnt) {
     HistArgs a{};
+    a.rows = rows;
+    a.rows_cnt = rows_cnt;
     a.keys = keys;
     a.table = table;
     a.n = (uint64_t)p.n;
@@ -300,9 +317,17 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
     // the first joint count of a sort clears the counts; a later one finds them cleared by the
     // copy-mode histogram that used them (or, where that pass fell back, is disabled by `enable`)
-    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4, s) != hipSuccess)
+    // (the rows counter sits after the joint counts: cleared with them)
+    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4 + 4, s) != hipSuccess)
         return RSORT_ERR_HIP;
-    if (launch_histogram_joint(a, s) != hipSuccess) return RSORT_ERR_HIP;
+    return hip_status(launch_histogram_joint(a, s));
+}
+
+// The next pass's chunks from the joint counts (rs_joint_bounds), after this pass's table is scanned
+// (ctab: a cut plan's pieces become row tasks where every chunk wrote its rows).
+int do_joint_bounds(const rsort_plan &p, const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
+                    uint32_t *plan, uint32_t *pcounts, const uint32_t *ctab, uint32_t *rows_cnt, hipStream_t s) {
+    PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
     // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
     // group boundary up to half a tile (and a quarter chunk) away
     const uint32_t snap = (uint32_t)std::min<int64_t>(p.tile_keys / 2, p.n / (4 * (int64_t)kJointBins));
@@ -310,15 +335,17 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     // (rs_joint_bounds; RSORT_CUT_WEIGHTS=0 turns it off for A/B runs)
     const uint32_t weighted = (enable == nullptr && cut_weights()) ? 1u : 0u;
     return hip_status(launch_joint_bounds(joint, enable, bounds, plan, pcounts, (uint64_t)p.n,
-                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, weighted, s));
+                                          (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, weighted, s,
+                                          ctab, rows_cnt));
 }
 
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                  int dmode, const uint32_t *split, int nsplit, hipStream_t s,
                  const uint32_t *bounds = nullptr, uint32_t *copy_src = nullptr,
                  const uint32_t *plan = nullptr, uint32_t *pcounts = nullptr, uint32_t *zero = nullptr,
-                 uint32_t *done = nullptr) {
+                 uint32_t *done = nullptr, uint32_t *rows = nullptr) {
     HistArgs a{};
+    a.rows = rows;
     a.zero = zero;
     a.zero_n = zero ? (uint64_t)p.table_entries : 0u;
     a.done = done;
@@ -466,6 +493,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // (raw tables only up to kRawTableMaxChunks chunks: each workgroup reads the whole table)
     const bool rawt = nextc && !nx_tail() && p.num_chunks <= kRawTableMaxChunks;
     uint32_t *const rot[3] = {c.table, c.table2, c.table3};
+    uint32_t *const rows = piece_rows() ? c.rows : nullptr, *const rows_cnt = rows ? c.rows_cnt : nullptr;
     for (int i = 0; i < P; ++i) {
         const int shift = i * p.k_bits;
         const bool to_out = ((P - 1 - i) % 2) == 0;  // the last pass always lands in `out`
@@ -479,14 +507,14 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         uint32_t *tab = rawt ? rot[i % 3] : (nextc && (i % 2 == 1)) ? c.table2 : c.table;
         uint32_t *nxt = (nextc && i + 1 < P) ? (rawt ? rot[(i + 1) % 3] : (i % 2 == 1) ? c.table : c.table2) : nullptr;
         uint32_t *clr = (rawt && i + 2 < P) ? rot[(i + 2) % 3] : nullptr;  // for the pass after next
+        const uint32_t *enable = (count_joint && i >= 2) ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
         if (count_joint) {
-            const uint32_t *enable = i >= 2 ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
-            if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable,
-                                         c.bounds + (i / 2) * kBoundsWords, c.plan, c.pcounts, s, i == 0)))
+            if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable, s, i == 0, rows, rows_cnt)))
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
-                                      c.pcounts, rawt ? nxt : nullptr, rawt ? c.done : nullptr))) {
+                                      c.pcounts, rawt ? nxt : nullptr, rawt ? c.done : nullptr,
+                                      bounds ? rows : nullptr))) {
             return st;
         }
         // next-digit plans: pass 0's table is scanned by launches (which also arm the tail counter;
@@ -494,6 +522,10 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         // previous scatter's last workgroup (raw tables: by every workgroup of the pass itself)
         if (!(nextc && i > 0) && !rawt &&
             (st = do_scan(p, tab, c.bsums, s, nxt, nextc ? c.done : nullptr, bounds ? &c : nullptr, bounds)))
+            return st;
+        // the next pass's chunks (after the scan: a cut plan finds the previous chunks' positions in it)
+        if (count_joint && (st = do_joint_bounds(p, c.joint, enable, c.bounds + (i / 2) * kBoundsWords, c.plan,
+                                                 c.pcounts, tab, rows_cnt, s)))
             return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
         // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the

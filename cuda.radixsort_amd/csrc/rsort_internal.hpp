@@ -89,6 +89,13 @@ struct HistArgs {
     uint32_t *zero;
     uint64_t zero_n;
     uint32_t *done;
+    // joint-count histograms: != nullptr -> a workgroup whose chunk is skewed (a digit holds more
+    // than twice its share) or that follows a cut plan (*joint_enable == kGroupsCut) also writes its
+    // joint counts as rows[c][digit][next digit] (R x R words per chunk) and bumps *rows_cnt; a cut
+    // plan made when every chunk wrote them takes its pieces' counts from the rows (rs_joint_bounds).
+    // Piece-mode launches: the rows the plan's row tasks sum.
+    uint32_t *rows;
+    uint32_t *rows_cnt;
 };
 
 struct ScatterArgs {
@@ -167,26 +174,49 @@ constexpr uint32_t kBoundsWords = kJointBins + 2;  // {flag, chunk starts[0..R]}
 //                 but its largest are counted from the keys ("pieces"), the largest is its
 //                 joint column minus the others, every whole group in a chunk is its joint column.
 constexpr uint32_t kGroupsFixed = 0, kGroupsWhole = 1, kGroupsCut = 2;
-// Cut plan (workspace, rs_joint_bounds): header {pieces, counted keys}, per chunk c a descriptor
-// {first group gA | last group gB << 8 | head mode << 16 | tail mode << 18 | empty << 20} (head:
-// chunk c's part of gA, slot 2c; tail: its part of gB != gA, slot 2c + 1), per cut group
-// {first chunk | last chunk << 8 | derived slot << 16}, and the pieces {start, end, slot, offset
-// among the counted keys}. pcounts: kPieceSlots rows of R digit counts, one per slot.
+// Cut plan (workspace, rs_joint_bounds): header {key ranges, counted keys, row tasks}, per chunk c a
+// descriptor {first group gA | last group gB << 8 | head mode << 16 | tail mode << 18 | empty << 20}
+// (head: chunk c's part of gA, slot 2c; tail: its part of gB != gA, slot 2c + 1), per cut group
+// {first chunk | last chunk << 8 | derived slot << 16}, the key ranges counted from the keys {start,
+// end, slot | kPieceNeg if counted negatively | derived slot << 16, offset among the counted keys}, and
+// the row tasks {slot | derived slot << 16, group, first chunk, end chunk}: a counted piece (a cut
+// group's part of a chunk, but the group's largest) is the keys of the previous pass's chunks [first,
+// end) in that group -- the sum of their joint-count rows (HistArgs::rows) -- plus or minus the keys at
+// its two ends (key ranges); without rows the whole piece is one key range. pcounts: kPieceSlots rows
+// of R digit counts, one per slot (mod 2^32: a negative range may take a row below zero for a while).
 constexpr uint32_t kSegWhole = 0, kSegCounted = 1, kSegDerived = 2;
 constexpr uint32_t kPlanDesc = 16;
 constexpr uint32_t kPlanGroup = kPlanDesc + kJointBins;
 constexpr uint32_t kPlanPieces = kPlanGroup + kJointBins;
-constexpr uint32_t kPlanWords = kPlanPieces + 4 * kJointBins;
+constexpr uint32_t kPlanMaxRanges = 4 * kJointBins;  // (<= 255 counted pieces, <= 2 key ranges each)
+constexpr uint32_t kPlanRows = kPlanPieces + 4 * kPlanMaxRanges;
+constexpr uint32_t kPlanWords = kPlanRows + 4 * kJointBins;
 constexpr uint32_t kPieceSlots = 2 * kJointBins;
+constexpr uint32_t kPieceNeg = 0x8000u;  // key range flag (slot word): counted negatively
+// joint-count rows: R chunks x R digits x R next digits (64 MiB), and the spills one chunk's rows can
+// hold in LDS (a 16-bit counter spills every 2^15 keys: chunk_keys / 2^15 <= 512 at n < 2^32)
+constexpr uint64_t kRowsWords = (uint64_t)kJointBins * kJointBins * kJointBins;
+constexpr uint32_t kMaxRowSpills = 512;
+// Upper bound of what a digit-group plan's workspace holds beyond any other plan's of the same n (the
+// joint counts, bounds, cut plan, piece counts and rows, each 256-B aligned): a caller that sizes a
+// workspace for one n and sorts a smaller one (the multi-GPU local sort) adds it.
+constexpr size_t kJointExtraBytes = ((size_t)kJointBins * kJointBins * 4 + 4 + 255) / 256 * 256 +
+                                    ((size_t)2 * kBoundsWords * 4 + 255) / 256 * 256 +
+                                    ((size_t)kPlanWords * 4 + 255) / 256 * 256 +
+                                    ((size_t)kPieceSlots * kJointBins * 4 + 255) / 256 * 256 +
+                                    (size_t)kRowsWords * 4;
 hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
 // From the joint counts [next digit][group]: the next pass's chunks into bounds[1..R+1] and its
 // mode into bounds[0] (above): kGroupsWhole when every group fits in max_keys keys, else the cut
 // plan (plan, pcounts rows zeroed); kGroupsFixed when the counts do not add up to n or enable
 // says the joint count was off (HistArgs::joint_enable). weighted != 0: a cut plan's chunks get
 // equal estimated cost instead of equal key counts (rs_joint_bounds).
+// ctab: the counting pass's scanned table; rows_cnt: HistArgs::rows_cnt (read and re-armed here) --
+// both given and every chunk's rows written: the cut plan's pieces are row tasks + their end keys.
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
-                               uint32_t snap, uint32_t weighted, hipStream_t s);
+                               uint32_t snap, uint32_t weighted, hipStream_t s,
+                               const uint32_t *ctab = nullptr, uint32_t *rows_cnt = nullptr);
 // rank_algo: internal RankAlgo. aligned16: the whole-line kernels may run -- keys-only: always
 // (any 4-B-aligned kout; launch_scatter shifts positions to kout's 128-B-aligned base); pairs: when
 // (vout - kout) % 16 == 0 (otherwise the same plan runs rs_scatter with the same tiles).

@@ -428,9 +428,17 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     constexpr uint32_t RS = R / 2 + 1;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t *s_sp = s_j + R * RS;
+    // HistArgs::rows: the spilled pairs (each spill moved 2^15 of the pair's count out of LDS) and the
+    // largest digit count of the chunk
+    __shared__ uint32_t s_spl[kMaxRowSpills];
+    __shared__ uint32_t s_nsp, s_rmax;
     const uint32_t t = threadIdx.x;
     RS_WG_T0
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
+    if (t == 0) {
+        s_nsp = 0u;
+        s_rmax = 0u;
+    }
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
     // add inc (<= 64) to the 16-bit counter of pair (d, e); the add that takes it to 2^15 moves 2^15
@@ -442,6 +450,10 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             atomicSub(&s_j[wi], 0x8000u << sh);
             atomicAdd(&s_sp[d], 0x8000u);
             atomicAdd(&a.joint[e * R + d], 0x8000u);
+            if (a.rows != nullptr) {
+                const uint32_t k = atomicAdd(&s_nsp, 1u);
+                if (k < kMaxRowSpills) s_spl[k] = d * R + e;
+            }
         }
     };
     auto add = [&](uint32_t x) { add_pair((x >> s0) & (R - 1u), (x >> s1) & (R - 1u), 1u); };
@@ -520,12 +532,41 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         }
         if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = s;
         else if (s) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], s);
+        if (a.rows != nullptr) atomicMax(&s_rmax, s);
     }
     // joint counts -> global [e][d] (consecutive lanes: consecutive d, one contiguous 256-B add)
     for (uint32_t item = t; item < R * R; item += THREADS) {
         const uint32_t e = item / R, d = item % R;
         const uint32_t v = (s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu;
         if (v) atomicAdd(&a.joint[item], v);
+    }
+    if (a.rows != nullptr && S == 1) {
+        // this chunk's joint counts as rows [digit][next digit] for a cut plan's pieces (HistArgs::rows):
+        // when the previous odd pass cut its groups (skewed keys: the next one likely cuts too) or a
+        // digit holds more than twice its share of the chunk; uniform chunks write nothing
+        __syncthreads();
+        const bool after_cut = a.joint_enable != nullptr && *a.joint_enable == kGroupsCut;
+        if ((after_cut || (uint64_t)s_rmax * R > 2 * (cend - cbeg)) && s_nsp <= kMaxRowSpills) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            uint32_t *rw = a.rows + (uint64_t)c * R * R;
+            for (uint32_t item = t; item < R * (R / 2); item += THREADS) {
+                const uint32_t d = item / (R / 2), j = item % (R / 2);
+                const uint32_t x = s_j[d * RS + j];
+                *reinterpret_cast<u32x2 *>(rw + d * R + 2 * j) = u32x2{x & 0xFFFFu, x >> 16};
+            }
+            // the spilled pairs: stored again with their spilled 2^15s on top, after every wave's row
+            // stores have reached the L2 (same workgroup, same L2: the later store wins; no release
+            // fence -- an agent-scope one writes the whole L2 back)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            for (uint32_t i = t; i < s_nsp; i += THREADS) {
+                const uint32_t pr = s_spl[i], d = pr / R, e = pr % R;
+                uint32_t k = 0;
+                for (uint32_t x = 0; x < s_nsp; ++x) k += s_spl[x] == pr ? 1u : 0u;
+                rw[pr] = ((s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu) + 0x8000u * k;
+            }
+            if (t == 0) atomicAdd(a.rows_cnt, 1u);
+        }
     }
     RS_WG_TH1;
 }
@@ -539,7 +580,7 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     constexpr uint32_t PLAIN = HW * R * SB;
     constexpr uint32_t JW = kJointBins * (kJointBins / 2 + 1) + kJointBins;
     static_assert(!JOINT || (BITS == kJointBits && DMODE == kDigitShift), "joint counts: k = 8 digits");
-    __shared__ uint32_t s_h[(JOINT && JW > PLAIN) ? JW : PLAIN];
+    __shared__ __attribute__((aligned(16))) uint32_t s_h[(JOINT && JW > PLAIN) ? JW : PLAIN];
 
     const uint32_t t = threadIdx.x;
     const uint32_t S = a.split;
@@ -640,7 +681,45 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
             // counts its share of every piece it meets, adds the counts into the piece's row and
             // takes them from its group's derived row (zeroed; the scan adds the joint counts)
             __shared__ uint32_t s_first;
-            const uint32_t np = a.plan[0], K = a.plan[1];
+            const uint32_t np = a.plan[0], K = a.plan[1], nr = a.plan[2];
+            // row tasks (rs_joint_bounds with HistArgs::rows): task i by workgroup i mod the grid -- the
+            // piece's whole previous chunks, their rows summed (THREADS / R threads per next digit)
+            if (nr > 0) {
+                // 64 threads per row (16-B loads), NQ rows at a time, 4 loads in flight per thread; the
+                // NQ partial rows summed through s_h (zero again before the keys are counted into it)
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                constexpr uint32_t NQ = THREADS / kWave;
+                static_assert(R == 4 * kWave && NQ * R <= PLAIN, "a row is one wave of quads");
+                const uint32_t q = t / kWave, e4 = lane_id();
+                for (uint32_t i = blockIdx.x; i < nr; i += gridDim.x) {
+                    const uint32_t *rt = a.plan + kPlanRows + 4 * i;
+                    const uint32_t sl = rt[0], g = rt[1], c0 = rt[2], c1 = rt[3];
+                    const u32x4 *rows4 = reinterpret_cast<const u32x4 *>(a.rows + (uint64_t)g * R) + e4;
+                    constexpr uint64_t CS = (uint64_t)R * R / 4;  // quads per chunk
+                    u32x4 acc = {0u, 0u, 0u, 0u};
+                    uint32_t cc = c0 + q;
+                    for (; cc + 3 * NQ < c1; cc += 4 * NQ) {
+                        const u32x4 v0 = rows4[cc * CS], v1 = rows4[(cc + NQ) * CS], v2 = rows4[(cc + 2 * NQ) * CS],
+                                    v3 = rows4[(cc + 3 * NQ) * CS];
+                        acc += v0 + v1 + v2 + v3;
+                    }
+                    for (; cc < c1; cc += NQ) acc += rows4[cc * CS];
+                    *reinterpret_cast<u32x4 *>(&s_h[q * R + 4 * e4]) = acc;
+                    __syncthreads();
+                    if (t < R) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (uint32_t x = 0; x < NQ; ++x) v += s_h[x * R + t];
+                        if (v) {
+                            atomicAdd(&a.pcounts[(sl & (kPieceNeg - 1u)) * R + t], v);
+                            atomicSub(&a.pcounts[(sl >> 16) * R + t], v);  // the group's derived segment
+                        }
+                    }
+                    __syncthreads();
+                }
+                for (uint32_t i = t; i < NQ * R; i += THREADS) s_h[i] = 0;
+                __syncthreads();
+            }
             const uint64_t s0 = (uint64_t)K * blockIdx.x / gridDim.x, s1 = (uint64_t)K * (blockIdx.x + 1) / gridDim.x;
             if (s0 >= s1) return;
             if (t < np) {
@@ -652,7 +731,8 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
             for (uint32_t i = s_first; i < np; ++i) {
                 const uint32_t ps = a.plan[kPlanPieces + 4 * i], pe = a.plan[kPlanPieces + 4 * i + 1];
                 const uint32_t sl = a.plan[kPlanPieces + 4 * i + 2], off = a.plan[kPlanPieces + 4 * i + 3];
-                const uint32_t slot = sl & 0xFFFFu, dslot = sl >> 16;
+                const uint32_t slot = sl & (kPieceNeg - 1u), dslot = sl >> 16;
+                const bool neg = (sl & kPieceNeg) != 0u;  // (a range the piece does NOT hold, rs_joint_bounds)
                 if (off >= s1) break;
                 const uint64_t lo = max(s0, (uint64_t)off), hi = min(s1, (uint64_t)off + (pe - ps));
                 count_range(ps + (lo - off), ps + (hi - off));
@@ -660,8 +740,8 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
                 for (uint32_t d = t; d < R; d += THREADS) {
                     const uint32_t v = take(d);
                     if (v) {
-                        atomicAdd(&a.pcounts[slot * R + d], v);
-                        atomicSub(&a.pcounts[dslot * R + d], v);  // the group's derived segment
+                        atomicAdd(&a.pcounts[slot * R + d], neg ? 0u - v : v);
+                        atomicSub(&a.pcounts[dslot * R + d], neg ? 0u - v : v);  // the group's derived segment
                     }
                 }
                 __syncthreads();
@@ -919,7 +999,8 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
 __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, const uint32_t *enable,
                                                         uint32_t *bounds, uint32_t *plan, uint32_t *pcounts,
                                                         uint64_t n, uint64_t max_keys, uint32_t snap,
-                                                        uint32_t weighted) {
+                                                        uint32_t weighted, const uint32_t *ctab,
+                                                        uint32_t *rows_cnt) {
     constexpr uint32_t R = kJointBins;
     constexpr uint32_t Q = 1024 / R;
     __shared__ uint32_t s_part[Q][R];
@@ -934,7 +1015,13 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     __shared__ unsigned long long s_big[R];        // cut group: largest segment (size << 10 | slot)
     __shared__ uint32_t s_cf[R], s_cl[R];          // cut group: first and last chunk
     __shared__ uint32_t s_slot[R];                 // counted pieces' slots
+    __shared__ uint32_t s_rows;                    // every chunk wrote its joint-count rows
     const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        // (read and re-armed for the next joint count; the other threads read s_rows after a barrier)
+        s_rows = (rows_cnt != nullptr && ctab != nullptr && *rows_cnt == R) ? 1u : 0u;
+        if (rows_cnt != nullptr) *rows_cnt = 0u;
+    }
     if (enable != nullptr && *enable == kGroupsFixed) {  // no joint count this pass
         if (t == 0) bounds[0] = kGroupsFixed;
         return;
@@ -1083,42 +1170,114 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     uint32_t hm = kSegWhole, tm = kSegWhole;
     if (hpart) hm = (uint32_t)(s_big[gA] & 1023u) == 2u * t ? kSegDerived : kSegCounted;
     if (tpart) tm = (uint32_t)(s_big[gB] & 1023u) == 2u * t + 1u ? kSegDerived : kSegCounted;
+    // a counted piece [ps, pe) of group g: with rows, the previous pass's chunks wholly inside it are a
+    // row task (chunk c's keys of group g sit at ctab[g][c] .. ctab[g][c + 1], the scanned table) and
+    // only its two ends are key ranges -- each end, or the rest of the chunk it lies in when that is
+    // shorter (the chunk's row then joins the task and the rest is counted negatively: a hot key's run
+    // can fill a whole chunk's part of its group); else one key range
+    struct Split {
+        uint32_t b[2], e[2], neg[2];  // key ranges [b, e), counted negatively where neg
+        uint32_t c0, c1;              // rows of chunks [c0, c1)
+    };
+    const bool rows = s_rows != 0u;
+    auto split = [&](uint32_t g, uint32_t ps, uint32_t pe) {
+        Split sp{{ps, pe}, {pe, pe}, {0u, 0u}, 0u, 0u};
+        if (!rows) return sp;
+        const uint32_t *row = ctab + (uint64_t)g * R;
+        const uint32_t gend = s_b[g + 1];
+        auto P = [&](uint32_t cc) { return cc < R ? row[cc] : gend; };
+        uint32_t lo = 0, hi = R;  // first boundary >= ps
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (P(mid) >= ps) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t c0 = lo;
+        lo = 0;
+        hi = R;  // last boundary <= pe
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (P(mid) <= pe) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t c1 = lo;
+        if (c0 <= c1) {
+            // whole chunks [c0, c1); the left end [ps, P(c0)) lies in chunk c0 - 1, the right end
+            // [P(c1), pe) in chunk c1
+            sp = Split{{ps, P(c1)}, {P(c0), pe}, {0u, 0u}, c0, c1};
+            if (c0 > 0 && ps - P(c0 - 1) < P(c0) - ps) sp = Split{{P(c0 - 1), P(c1)}, {ps, pe}, {1u, 0u}, c0 - 1, c1};
+            if (c1 < R && P(c1 + 1) - pe < pe - P(c1)) {
+                sp.b[1] = pe;
+                sp.e[1] = P(c1 + 1);
+                sp.neg[1] = 1u;
+                sp.c1 = c1 + 1;
+            }
+        } else if (P(c0) - P(c1) < 2 * (pe - ps)) {
+            // inside chunk c1 = c0 - 1, and its rest is the shorter: its row less the two rest ranges
+            sp = Split{{P(c1), pe}, {ps, P(c0)}, {1u, 1u}, c1, c0};
+        }
+        return sp;
+    };
+    Split hs{{0u, 0u}, {0u, 0u}, {0u, 0u}, 0u, 0u}, ts = hs;
+    if (hm == kSegCounted) hs = split(gA, hb, he);
+    if (tm == kSegCounted) ts = split(gB, tb, te);
     const uint32_t npc = (hm == kSegCounted ? 1u : 0u) + (tm == kSegCounted ? 1u : 0u);
-    const uint32_t nkc = (hm == kSegCounted ? he - hb : 0u) + (tm == kSegCounted ? te - tb : 0u);
-    uint32_t np = 0, K = 0;
-    uint32_t pi = block_excl_scan<1024>(npc, s_ws, np);
+    auto nranges = [](const Split &x) { return (x.e[0] > x.b[0] ? 1u : 0u) + (x.e[1] > x.b[1] ? 1u : 0u); };
+    auto nkeys = [](const Split &x) {
+        return (x.e[0] > x.b[0] ? x.e[0] - x.b[0] : 0u) + (x.e[1] > x.b[1] ? x.e[1] - x.b[1] : 0u);
+    };
+    const uint32_t nrg = nranges(hs) + nranges(ts);
+    const uint32_t nkc = nkeys(hs) + nkeys(ts);
+    const uint32_t nrt = (hs.c1 > hs.c0 ? 1u : 0u) + (ts.c1 > ts.c0 ? 1u : 0u);
+    uint32_t np = 0, K = 0, nr = 0, npieces = 0;
+    uint32_t pi = block_excl_scan<1024>(npc, s_ws, npieces);
+    uint32_t gi = block_excl_scan<1024>(nrg, s_ws, np);
     uint32_t ko = block_excl_scan<1024>(nkc, s_ws, K);
+    uint32_t ri = block_excl_scan<1024>(nrt, s_ws, nr);
     if (t < R) {
         plan[kPlanDesc + t] = gA | (gB << 8) | (hm << 16) | (tm << 18) | ((empty ? 1u : 0u) << 20);
         plan[kPlanGroup + t] = (s_cf[t] & 255u) | ((s_cl[t] & 255u) << 8) | ((uint32_t)(s_big[t] & 1023u) << 16);
+        auto emit = [&](const Split &x, uint32_t sl, uint32_t g) {
+            for (int i = 0; i < 2; ++i) {
+                if (x.e[i] <= x.b[i]) continue;
+                uint32_t *pc = plan + kPlanPieces + 4 * gi;
+                pc[0] = x.b[i];
+                pc[1] = x.e[i];
+                pc[2] = sl | (x.neg[i] ? kPieceNeg : 0u);
+                pc[3] = ko;
+                ++gi;
+                ko += x.e[i] - x.b[i];
+            }
+            if (x.c1 > x.c0) {
+                uint32_t *rt = plan + kPlanRows + 4 * ri;
+                rt[0] = sl;
+                rt[1] = g;
+                rt[2] = x.c0;
+                rt[3] = x.c1;
+                ++ri;
+            }
+        };
         if (hm == kSegCounted) {
-            uint32_t *pc = plan + kPlanPieces + 4 * pi;
-            pc[0] = hb;
-            pc[1] = he;
-            pc[2] = (2u * t) | ((uint32_t)(s_big[gA] & 1023u) << 16);
-            pc[3] = ko;
+            emit(hs, (2u * t) | ((uint32_t)(s_big[gA] & 1023u) << 16), gA);
             s_slot[pi] = 2u * t;
             ++pi;
-            ko += he - hb;
         }
         if (tm == kSegCounted) {
-            uint32_t *pc = plan + kPlanPieces + 4 * pi;
-            pc[0] = tb;
-            pc[1] = te;
-            pc[2] = (2u * t + 1u) | ((uint32_t)(s_big[gB] & 1023u) << 16);
-            pc[3] = ko;
+            emit(ts, (2u * t + 1u) | ((uint32_t)(s_big[gB] & 1023u) << 16), gB);
             s_slot[pi] = 2u * t + 1u;
         }
     }
+    np = min(np, kPlanMaxRanges);  // (cannot exceed it: <= 255 counted pieces, 2 ranges each)
     if (t == 0) {
         plan[0] = np;
         plan[1] = K;
+        plan[2] = nr;
         bounds[0] = kGroupsCut;
     }
     __syncthreads();
     // the counted pieces' rows and each cut group's derived row start at zero (the histogram
     // launch adds every piece's counts into its row and takes them from its group's derived row)
-    for (uint32_t i = t; i < np * R; i += 1024) pcounts[s_slot[i / R] * R + i % R] = 0u;
+    for (uint32_t i = t; i < npieces * R; i += 1024) pcounts[s_slot[i / R] * R + i % R] = 0u;
     for (uint32_t i = t; i < R * R; i += 1024) {
         const uint32_t gg = i / R, d = i % R;
         if (s_big[gg] != 0ull) pcounts[(uint32_t)(s_big[gg] & 1023u) * R + d] = 0u;
@@ -2968,8 +3127,10 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
 
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
-                               uint32_t snap, uint32_t weighted, hipStream_t s) {
-    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap, weighted);
+                               uint32_t snap, uint32_t weighted, hipStream_t s, const uint32_t *ctab,
+                               uint32_t *rows_cnt) {
+    rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap, weighted, ctab,
+                                       rows_cnt);
     return hipGetLastError();
 }
 

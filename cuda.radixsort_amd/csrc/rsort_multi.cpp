@@ -126,8 +126,10 @@ size_t sub_bytes(int64_t n, int64_t cap, int k, int pairs, int world) {
     // the gathered sample: world rows of at most kSampleBudget samples
     size_t b = rsort_workspace_size(world * kSampleBudget, 8, 0) + ((size_t)4 << 8 << 12);
     // the received count is only known later; a smaller n can pick a geometry with a larger
-    // chunk table (<= 2^k x 4096 entries), so leave room for that
-    size_t c = rsort_workspace_size(std::max<int64_t>(cap, 1), k, pairs) + ((size_t)4 << k << 12);
+    // chunk table (<= 2^k x 4096 entries), or a digit-group plan where cap's is not, so leave room
+    // for both
+    size_t c = rsort_workspace_size(std::max<int64_t>(cap, 1), k, pairs) + ((size_t)4 << k << 12) +
+               (k == kJointBits ? kJointExtraBytes : 0);
     return std::max(a, std::max(b, c));
 }
 

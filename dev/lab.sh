@@ -180,11 +180,11 @@ PY
     ;;
 envab)
     # the C3 line and a configs block (default c2) with and without an environment setting of the
-    # library, alternating twice: bash dev/lab.sh envab RSORT_NX_TAIL=1 [configs]
+    # library, alternating twice: bash dev/lab.sh envab "RSORT_LAB=1 RSORT_NX_TAIL=1" [configs]
     kv=$1
     for side in new env new env; do
         if [ "$side" = env ]; then
-            env "$kv" timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
+            env $kv timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
                 --configs "${2:-c2}" > gpurun_out/envab_$side.json 2> gpurun_out/envab_$side.err
         else
             timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \

@@ -157,6 +157,28 @@ def test_joint_counter_spill():
         assert np.array_equal(y, oracle_sort(x, 8))
 
 
+def test_cut_plan_rows_with_spills():
+    """A cut plan whose pieces come from the per-chunk joint-count rows (HistArgs::rows) while the
+    chunks. 16-bit joint counters spill: 60 % of the keys share digits 0 and 1 (>= 2^15 equal pairs per
+    workgroup: the rows take the spilled 2^15s on top), the rest uniform. Bit-exact against the oracle,
+    keys and pairs."""
+    for tiles, pairs in ((1024, False), (2048, True)):
+        n = tiles * (PAIRS_TILE if pairs else LINE_TILE) - 7
+        rng = np.random.default_rng(tiles)
+        x = uniform_keys(n, seed=tiles)
+        hot = rng.random(n) < 0.6
+        x[hot] = (x[hot] & np.uint32(0xFFFF0000)) | np.uint32(0x1234)
+        if pairs:
+            v = np.arange(n, dtype=np.uint32)
+            (ko, vo), flags = run(x, group_plan(n, pairs=True), vals=v)
+            wk, wv = oracle_sort_pairs(x, v, 8)
+            assert np.array_equal(ko, wk) and np.array_equal(vo, wv)
+        else:
+            y, flags = run(x, group_plan(n))
+            assert np.array_equal(y, oracle_sort(x, 8))
+        assert flags[0] == 2
+
+
 def test_empty_groups():
     """64 of the 256 digit-0 values never occur; the other groups still fit one tile over a chunk."""
     n = 512 * LINE_TILE
@@ -447,11 +469,13 @@ print("LAB " + " ".join(out))
 
 
 @pytest.mark.parametrize("env,feat4", [({"RSORT_LAB": "1", "RSORT_NX_TAIL": "1", "RSORT_CUT_WEIGHTS": "0"}, 2 | 8),
-                                       ({"RSORT_NX_TAIL": "1", "RSORT_CUT_WEIGHTS": "0"}, 2 | 4)])
+                                       ({"RSORT_NX_TAIL": "1", "RSORT_CUT_WEIGHTS": "0"}, 2 | 4),
+                                       ({"RSORT_LAB": "1", "RSORT_PIECE_ROWS": "0"}, 2 | 4)])
 def test_lab_switches_in_a_subprocess(env, feat4):
     """The A/B switches are read once per process, and only under RSORT_LAB=1: with
-    it, k = 3, 4 sorts take the tail scans (features) and the Zipf k = 8 sort equal-count cut plans;
-    without it the same variables change nothing. Both sort correctly."""
+    it, k = 3, 4 sorts take the tail scans (features) and the Zipf k = 8 sort equal-count cut plans
+    (or, RSORT_PIECE_ROWS=0, cut plans whose pieces are all counted from the keys); without it the
+    same variables change nothing. All sort correctly."""
     import os
     import subprocess
     import sys
