@@ -227,7 +227,7 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
         ws += align256((size_t)2 * kBoundsWords * 4);             // group bounds of passes 1 and 3
         ws += align256((size_t)kPlanWords * 4);                   // cut plan
         ws += align256((size_t)kPieceSlots * kJointBins * 4);     // its piece counts
-        ws += align256((size_t)kRowsWords * 4);                   // per-chunk joint-count rows (64 MiB)
+        ws += align256(((size_t)kRowsWords + kJointBins * kJointBins) * 4);  // per-chunk joint-count rows (64 MiB)
     }
     if (!partition && next_plan(*p)) {
         ws += align256((size_t)p->table_entries * 4);  // the next pass's table
@@ -279,7 +279,7 @@ Carve carve(const rsort_plan &p, void *ws) {
         c.pcounts = (uint32_t *)q;
         q += align256((size_t)kPieceSlots * kJointBins * 4);
         c.rows = (uint32_t *)q;
-        q += align256((size_t)kRowsWords * 4);
+        q += align256(((size_t)kRowsWords + kJointBins * kJointBins) * 4);
     }
     if (next_plan(p)) {
         c.table2 = (uint32_t *)q;
@@ -326,7 +326,8 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
 // The next pass's chunks from the joint counts (rs_joint_bounds), after this pass's table is scanned
 // (ctab: a cut plan's pieces become row tasks where every chunk wrote its rows).
 int do_joint_bounds(const rsort_plan &p, const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
-                    uint32_t *plan, uint32_t *pcounts, const uint32_t *ctab, uint32_t *rows_cnt, hipStream_t s) {
+                    uint32_t *plan, uint32_t *pcounts, const uint32_t *ctab, uint32_t *rows_cnt,
+                    const uint32_t *rowone, hipStream_t s) {
     PhaseScope ps(RSORT_PHASE_HISTOGRAM, p.n, s);
     // a group may take one tile more than a fixed chunk; a cut-plan chunk boundary moves to a
     // group boundary up to half a tile (and a quarter chunk) away
@@ -336,7 +337,7 @@ int do_joint_bounds(const rsort_plan &p, const uint32_t *joint, const uint32_t *
     const uint32_t weighted = (enable == nullptr && cut_weights()) ? 1u : 0u;
     return hip_status(launch_joint_bounds(joint, enable, bounds, plan, pcounts, (uint64_t)p.n,
                                           (uint64_t)p.chunk_keys + (uint64_t)p.tile_keys, snap, weighted, s,
-                                          ctab, rows_cnt));
+                                          ctab, rows_cnt, rowone));
 }
 
 int do_histogram(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
@@ -525,7 +526,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
             return st;
         // the next pass's chunks (after the scan: a cut plan finds the previous chunks' positions in it)
         if (count_joint && (st = do_joint_bounds(p, c.joint, enable, c.bounds + (i / 2) * kBoundsWords, c.plan,
-                                                 c.pcounts, tab, rows_cnt, s)))
+                                                 c.pcounts, tab, rows_cnt, rows ? rows + kRowsWords : nullptr, s)))
             return st;
         // passes after the first of a digit-group sort: where the previous odd pass's groups were
         // unbalanced (skewed, duplicate-heavy keys: runs of equal keys in this pass's input), the

@@ -179,7 +179,8 @@ constexpr uint32_t kGroupsFixed = 0, kGroupsWhole = 1, kGroupsCut = 2;
 // (head: chunk c's part of gA, slot 2c; tail: its part of gB != gA, slot 2c + 1), per cut group
 // {first chunk | last chunk << 8 | derived slot << 16}, the key ranges counted from the keys {start,
 // end, slot | kPieceNeg if counted negatively | derived slot << 16, offset among the counted keys}, and
-// the row tasks {slot | derived slot << 16, group, first chunk, end chunk}: a counted piece (a cut
+// the row tasks {slot | derived slot << 16, group, first chunk, end chunk} (or direct adds, kRowDirect:
+// an end inside a previous chunk whose keys of the group all have one next digit): a counted piece (a cut
 // group's part of a chunk, but the group's largest) is the keys of the previous pass's chunks [first,
 // end) in that group -- the sum of their joint-count rows (HistArgs::rows) -- plus or minus the keys at
 // its two ends (key ranges); without rows the whole piece is one key range. pcounts: kPieceSlots rows
@@ -190,11 +191,13 @@ constexpr uint32_t kPlanGroup = kPlanDesc + kJointBins;
 constexpr uint32_t kPlanPieces = kPlanGroup + kJointBins;
 constexpr uint32_t kPlanMaxRanges = 4 * kJointBins;  // (<= 255 counted pieces, <= 2 key ranges each)
 constexpr uint32_t kPlanRows = kPlanPieces + 4 * kPlanMaxRanges;
-constexpr uint32_t kPlanWords = kPlanRows + 4 * kJointBins;
+constexpr uint32_t kPlanWords = kPlanRows + 4 * 3 * kJointBins;  // (<= 3 tasks per counted piece)
+constexpr uint32_t kRowDirect = 0x80000000u;  // row task {slot, kRowDirect | next digit, keys, 0}: a direct add
 constexpr uint32_t kPieceSlots = 2 * kJointBins;
 constexpr uint32_t kPieceNeg = 0x8000u;  // key range flag (slot word): counted negatively
-// joint-count rows: R chunks x R digits x R next digits (64 MiB), and the spills one chunk's rows can
-// hold in LDS (a 16-bit counter spills every 2^15 keys: chunk_keys / 2^15 <= 512 at n < 2^32)
+// joint-count rows: R chunks x R digits x R next digits (64 MiB; then R x R words: each row's one
+// next digit, or ~0), and the spills one chunk's rows can hold in LDS (a 16-bit counter spills every
+// 2^15 keys: chunk_keys / 2^15 <= 512 at n < 2^32)
 constexpr uint64_t kRowsWords = (uint64_t)kJointBins * kJointBins * kJointBins;
 constexpr uint32_t kMaxRowSpills = 512;
 // Upper bound of what a digit-group plan's workspace holds beyond any other plan's of the same n (the
@@ -204,19 +207,21 @@ constexpr size_t kJointExtraBytes = ((size_t)kJointBins * kJointBins * 4 + 4 + 2
                                     ((size_t)2 * kBoundsWords * 4 + 255) / 256 * 256 +
                                     ((size_t)kPlanWords * 4 + 255) / 256 * 256 +
                                     ((size_t)kPieceSlots * kJointBins * 4 + 255) / 256 * 256 +
-                                    (size_t)kRowsWords * 4;
+                                    ((size_t)kRowsWords + kJointBins * kJointBins) * 4;
 hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s);
 // From the joint counts [next digit][group]: the next pass's chunks into bounds[1..R+1] and its
 // mode into bounds[0] (above): kGroupsWhole when every group fits in max_keys keys, else the cut
 // plan (plan, pcounts rows zeroed); kGroupsFixed when the counts do not add up to n or enable
 // says the joint count was off (HistArgs::joint_enable). weighted != 0: a cut plan's chunks get
 // equal estimated cost instead of equal key counts (rs_joint_bounds).
-// ctab: the counting pass's scanned table; rows_cnt: HistArgs::rows_cnt (read and re-armed here) --
-// both given and every chunk's rows written: the cut plan's pieces are row tasks + their end keys.
+// ctab: the counting pass's scanned table; rows_cnt: HistArgs::rows_cnt (read and re-armed here);
+// rowone: the rows' one-digit words (HistArgs::rows + kRowsWords) -- all given and every chunk's rows
+// written: the cut plan's pieces are row tasks + their end keys (or direct adds).
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
                                uint32_t snap, uint32_t weighted, hipStream_t s,
-                               const uint32_t *ctab = nullptr, uint32_t *rows_cnt = nullptr);
+                               const uint32_t *ctab = nullptr, uint32_t *rows_cnt = nullptr,
+                               const uint32_t *rowone = nullptr);
 // rank_algo: internal RankAlgo. aligned16: the whole-line kernels may run -- keys-only: always
 // (any 4-B-aligned kout; launch_scatter shifts positions to kout's 128-B-aligned base); pairs: when
 // (vout - kout) % 16 == 0 (otherwise the same plan runs rs_scatter with the same tiles).

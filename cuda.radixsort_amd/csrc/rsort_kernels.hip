@@ -432,6 +432,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     // largest digit count of the chunk
     __shared__ uint32_t s_spl[kMaxRowSpills];
     __shared__ uint32_t s_nsp, s_rmax;
+    __shared__ uint32_t s_nz[R], s_ne[R];  // per row: nonzero entries, and one of them
     const uint32_t t = threadIdx.x;
     RS_WG_T0
     for (uint32_t i = t; i < R * RS + R; i += THREADS) s_j[i] = 0;
@@ -439,6 +440,7 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         s_nsp = 0u;
         s_rmax = 0u;
     }
+    for (uint32_t i = t; i < R; i += THREADS) s_nz[i] = 0u;
     __syncthreads();
     const uint32_t s0 = a.shift, s1 = a.shift + kJointBits;
     // add inc (<= 64) to the 16-bit counter of pair (d, e); the add that takes it to 2^15 moves 2^15
@@ -553,6 +555,11 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
                 const uint32_t d = item / (R / 2), j = item % (R / 2);
                 const uint32_t x = s_j[d * RS + j];
                 *reinterpret_cast<u32x2 *>(rw + d * R + 2 * j) = u32x2{x & 0xFFFFu, x >> 16};
+                const uint32_t nz = ((x & 0xFFFFu) ? 1u : 0u) + ((x >> 16) ? 1u : 0u);
+                if (nz) {
+                    atomicAdd(&s_nz[d], nz);
+                    s_ne[d] = (x & 0xFFFFu) ? 2 * j : 2 * j + 1;
+                }
             }
             // the spilled pairs: stored again with their spilled 2^15s on top, after every wave's row
             // stores have reached the L2 (same workgroup, same L2: the later store wins; no release
@@ -562,9 +569,22 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
             for (uint32_t i = t; i < s_nsp; i += THREADS) {
                 const uint32_t pr = s_spl[i], d = pr / R, e = pr % R;
                 uint32_t k = 0;
-                for (uint32_t x = 0; x < s_nsp; ++x) k += s_spl[x] == pr ? 1u : 0u;
-                rw[pr] = ((s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu) + 0x8000u * k;
+                bool first = true;
+                for (uint32_t x = 0; x < s_nsp; ++x) {
+                    k += s_spl[x] == pr ? 1u : 0u;
+                    first = first && !(x < i && s_spl[x] == pr);
+                }
+                const uint32_t res = (s_j[d * RS + (e >> 1)] >> ((e & 1u) << 4)) & 0xFFFFu;
+                rw[pr] = res + 0x8000u * k;
+                if (first && res == 0u) {  // (a nonzero entry the row loop saw as zero)
+                    atomicAdd(&s_nz[d], 1u);
+                    s_ne[d] = e;
+                }
             }
+            __syncthreads();
+            // per row: its one next digit when it has exactly one (a piece end inside this chunk's part
+            // of that group then needs no key read, rs_joint_bounds), else ~0
+            for (uint32_t d = t; d < R; d += THREADS) a.rows[kRowsWords + (uint64_t)c * R + d] = s_nz[d] == 1u ? s_ne[d] : ~0u;
             if (t == 0) atomicAdd(a.rows_cnt, 1u);
         }
     }
@@ -694,6 +714,13 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
                 for (uint32_t i = blockIdx.x; i < nr; i += gridDim.x) {
                     const uint32_t *rt = a.plan + kPlanRows + 4 * i;
                     const uint32_t sl = rt[0], g = rt[1], c0 = rt[2], c1 = rt[3];
+                    if (g & kRowDirect) {  // (uniform: the whole workgroup skips the row sum)
+                        if (t == 0) {
+                            atomicAdd(&a.pcounts[(sl & (kPieceNeg - 1u)) * R + (g & (R - 1u))], c0);
+                            atomicSub(&a.pcounts[(sl >> 16) * R + (g & (R - 1u))], c0);
+                        }
+                        continue;
+                    }
                     const u32x4 *rows4 = reinterpret_cast<const u32x4 *>(a.rows + (uint64_t)g * R) + e4;
                     constexpr uint64_t CS = (uint64_t)R * R / 4;  // quads per chunk
                     u32x4 acc = {0u, 0u, 0u, 0u};
@@ -1000,7 +1027,7 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
                                                         uint32_t *bounds, uint32_t *plan, uint32_t *pcounts,
                                                         uint64_t n, uint64_t max_keys, uint32_t snap,
                                                         uint32_t weighted, const uint32_t *ctab,
-                                                        uint32_t *rows_cnt) {
+                                                        uint32_t *rows_cnt, const uint32_t *rowone) {
     constexpr uint32_t R = kJointBins;
     constexpr uint32_t Q = 1024 / R;
     __shared__ uint32_t s_part[Q][R];
@@ -1019,7 +1046,7 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     const uint32_t t = threadIdx.x;
     if (t == 0) {
         // (read and re-armed for the next joint count; the other threads read s_rows after a barrier)
-        s_rows = (rows_cnt != nullptr && ctab != nullptr && *rows_cnt == R) ? 1u : 0u;
+        s_rows = (rows_cnt != nullptr && ctab != nullptr && rowone != nullptr && *rows_cnt == R) ? 1u : 0u;
         if (rows_cnt != nullptr) *rows_cnt = 0u;
     }
     if (enable != nullptr && *enable == kGroupsFixed) {  // no joint count this pass
@@ -1178,10 +1205,11 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     struct Split {
         uint32_t b[2], e[2], neg[2];  // key ranges [b, e), counted negatively where neg
         uint32_t c0, c1;              // rows of chunks [c0, c1)
+        uint32_t dl[2], de[2];        // direct adds: dl keys of next digit de (an end in a one-digit row)
     };
     const bool rows = s_rows != 0u;
     auto split = [&](uint32_t g, uint32_t ps, uint32_t pe) {
-        Split sp{{ps, pe}, {pe, pe}, {0u, 0u}, 0u, 0u};
+        Split sp{{ps, pe}, {pe, pe}, {0u, 0u}, 0u, 0u, {0u, 0u}, {0u, 0u}};
         if (!rows) return sp;
         const uint32_t *row = ctab + (uint64_t)g * R;
         const uint32_t gend = s_b[g + 1];
@@ -1201,24 +1229,47 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
             else hi = mid - 1;
         }
         const uint32_t c1 = lo;
+        auto one = [&](uint32_t cc) { return rowone[(uint64_t)cc * R + g]; };  // chunk cc's row: its one digit
         if (c0 <= c1) {
             // whole chunks [c0, c1); the left end [ps, P(c0)) lies in chunk c0 - 1, the right end
-            // [P(c1), pe) in chunk c1
-            sp = Split{{ps, P(c1)}, {P(c0), pe}, {0u, 0u}, c0, c1};
-            if (c0 > 0 && ps - P(c0 - 1) < P(c0) - ps) sp = Split{{P(c0 - 1), P(c1)}, {ps, pe}, {1u, 0u}, c0 - 1, c1};
-            if (c1 < R && P(c1 + 1) - pe < pe - P(c1)) {
-                sp.b[1] = pe;
-                sp.e[1] = P(c1 + 1);
-                sp.neg[1] = 1u;
-                sp.c1 = c1 + 1;
+            // [P(c1), pe) in chunk c1 (P(0) <= ps and pe <= P(R): the chunks exist when the ends do)
+            sp = Split{{ps, P(c1)}, {P(c0), pe}, {0u, 0u}, c0, c1, {0u, 0u}, {0u, 0u}};
+            if (ps < P(c0)) {
+                const uint32_t e1 = one(c0 - 1);
+                if (e1 < R) {
+                    sp.dl[0] = P(c0) - ps;
+                    sp.de[0] = e1;
+                    sp.b[0] = sp.e[0];
+                } else if (ps - P(c0 - 1) < P(c0) - ps) {
+                    sp.b[0] = P(c0 - 1);
+                    sp.e[0] = ps;
+                    sp.neg[0] = 1u;
+                    sp.c0 = c0 - 1;
+                }
             }
+            if (pe > P(c1)) {
+                const uint32_t e2 = one(c1);
+                if (e2 < R) {
+                    sp.dl[1] = pe - P(c1);
+                    sp.de[1] = e2;
+                    sp.b[1] = sp.e[1];
+                } else if (P(c1 + 1) - pe < pe - P(c1)) {
+                    sp.b[1] = pe;
+                    sp.e[1] = P(c1 + 1);
+                    sp.neg[1] = 1u;
+                    sp.c1 = c1 + 1;
+                }
+            }
+        } else if (one(c1) < R) {
+            // inside chunk c1 = c0 - 1, whose keys of group g all have one next digit
+            sp = Split{{pe, pe}, {pe, pe}, {0u, 0u}, 0u, 0u, {pe - ps, 0u}, {one(c1), 0u}};
         } else if (P(c0) - P(c1) < 2 * (pe - ps)) {
-            // inside chunk c1 = c0 - 1, and its rest is the shorter: its row less the two rest ranges
-            sp = Split{{P(c1), pe}, {ps, P(c0)}, {1u, 1u}, c1, c0};
+            // inside chunk c1, and its rest is the shorter: its row less the two rest ranges
+            sp = Split{{P(c1), pe}, {ps, P(c0)}, {1u, 1u}, c1, c0, {0u, 0u}, {0u, 0u}};
         }
         return sp;
     };
-    Split hs{{0u, 0u}, {0u, 0u}, {0u, 0u}, 0u, 0u}, ts = hs;
+    Split hs{{0u, 0u}, {0u, 0u}, {0u, 0u}, 0u, 0u, {0u, 0u}, {0u, 0u}}, ts = hs;
     if (hm == kSegCounted) hs = split(gA, hb, he);
     if (tm == kSegCounted) ts = split(gB, tb, te);
     const uint32_t npc = (hm == kSegCounted ? 1u : 0u) + (tm == kSegCounted ? 1u : 0u);
@@ -1228,7 +1279,10 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     };
     const uint32_t nrg = nranges(hs) + nranges(ts);
     const uint32_t nkc = nkeys(hs) + nkeys(ts);
-    const uint32_t nrt = (hs.c1 > hs.c0 ? 1u : 0u) + (ts.c1 > ts.c0 ? 1u : 0u);
+    auto ntasks = [](const Split &x) {
+        return (x.c1 > x.c0 ? 1u : 0u) + (x.dl[0] > 0u ? 1u : 0u) + (x.dl[1] > 0u ? 1u : 0u);
+    };
+    const uint32_t nrt = ntasks(hs) + ntasks(ts);
     uint32_t np = 0, K = 0, nr = 0, npieces = 0;
     uint32_t pi = block_excl_scan<1024>(npc, s_ws, npieces);
     uint32_t gi = block_excl_scan<1024>(nrg, s_ws, np);
@@ -1254,6 +1308,15 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
                 rt[1] = g;
                 rt[2] = x.c0;
                 rt[3] = x.c1;
+                ++ri;
+            }
+            for (int i = 0; i < 2; ++i) {
+                if (x.dl[i] == 0u) continue;
+                uint32_t *rt = plan + kPlanRows + 4 * ri;  // a direct add: dl keys of next digit de
+                rt[0] = sl;
+                rt[1] = kRowDirect | x.de[i];
+                rt[2] = x.dl[i];
+                rt[3] = 0u;
                 ++ri;
             }
         };
@@ -3128,9 +3191,9 @@ hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
 hipError_t launch_joint_bounds(const uint32_t *joint, const uint32_t *enable, uint32_t *bounds,
                                uint32_t *plan, uint32_t *pcounts, uint64_t n, uint64_t max_keys,
                                uint32_t snap, uint32_t weighted, hipStream_t s, const uint32_t *ctab,
-                               uint32_t *rows_cnt) {
+                               uint32_t *rows_cnt, const uint32_t *rowone) {
     rs_joint_bounds<<<1, 1024, 0, s>>>(joint, enable, bounds, plan, pcounts, n, max_keys, snap, weighted, ctab,
-                                       rows_cnt);
+                                       rows_cnt, rowone);
     return hipGetLastError();
 }
 
