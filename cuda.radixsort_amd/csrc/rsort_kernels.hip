@@ -551,14 +551,18 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
         if ((after_cut || (uint64_t)s_rmax * R > 2 * (cend - cbeg)) && s_nsp <= kMaxRowSpills) {
             typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
             uint32_t *rw = a.rows + (uint64_t)c * R * R;
+            static_assert(THREADS % kWave == 0 && (R / 2) % kWave == 0, "a wave's items lie in one row");
             for (uint32_t item = t; item < R * (R / 2); item += THREADS) {
                 const uint32_t d = item / (R / 2), j = item % (R / 2);
                 const uint32_t x = s_j[d * RS + j];
                 *reinterpret_cast<u32x2 *>(rw + d * R + 2 * j) = u32x2{x & 0xFFFFu, x >> 16};
-                const uint32_t nz = ((x & 0xFFFFu) ? 1u : 0u) + ((x >> 16) ? 1u : 0u);
-                if (nz) {
+                // the row's nonzero entries, one LDS add per wave (its 64 items share the row)
+                const uint64_t blo = __ballot((x & 0xFFFFu) != 0u), bhi = __ballot((x >> 16) != 0u);
+                const uint32_t nz = wave_count(blo) + wave_count(bhi);
+                if (nz != 0u && lane_id() == 0) {
+                    const uint32_t j0 = j;  // (lane 0's item: the wave's first)
                     atomicAdd(&s_nz[d], nz);
-                    s_ne[d] = (x & 0xFFFFu) ? 2 * j : 2 * j + 1;
+                    s_ne[d] = blo ? 2 * (j0 + (uint32_t)__builtin_ctzll(blo)) : 2 * (j0 + (uint32_t)__builtin_ctzll(bhi)) + 1;
                 }
             }
             // the spilled pairs: stored again with their spilled 2^15s on top, after every wave's row
