@@ -341,7 +341,7 @@ def run_config(name, c, dev, reps, n_override=0, cpu_n=0, cpu_reps=3):
     rs.scatter_kernels_used(reset=True)
     # warm-up by time, not count: a config runs after host-side work (the end-to-end copy, the CPU
     # rows) that leaves the GPU idle and its clocks down, and two 1-ms sorts (C2) do not bring them
-    # back (the same C2 library ran 1.058 ms/sort here against 0.98-0.99 in runs without that idle
+    # back (the same C2 library: 1.058 ms/sort in this block, 0.98-0.99 in runs without that idle
     # time); >= 0.25 s of sorts first, at least 2
     t0 = time.perf_counter()
     for i in range(400):
