@@ -179,6 +179,27 @@ def test_cut_plan_rows_with_spills():
         assert flags[0] == 2
 
 
+@pytest.mark.parametrize("pairs", [False, True])
+def test_cut_plan_rows_hot_key_runs(pairs):
+    """40 % of the keys one value, the rest uniform: both odd passes cut (the hot key's digit 0 and
+    digit 2 groups). Pass 3's pieces end inside previous chunks that hold nothing but the hot key's
+    copies (one next digit: direct adds, no key read) and pass 1's inside mixed ones (key ranges, or
+    their complements counted negatively). Bit-exact against the oracle."""
+    n = 768 * (PAIRS_TILE if pairs else LINE_TILE) - 3
+    rng = np.random.default_rng(77)
+    x = uniform_keys(n, seed=77)
+    x[rng.random(n) < 0.4] = np.uint32(0x9E3779B9)
+    if pairs:
+        v = np.arange(n, dtype=np.uint32)
+        (ko, vo), flags = run(x, group_plan(n, pairs=True), vals=v)
+        wk, wv = oracle_sort_pairs(x, v, 8)
+        assert np.array_equal(ko, wk) and np.array_equal(vo, wv)
+    else:
+        y, flags = run(x, group_plan(n))
+        assert np.array_equal(y, oracle_sort(x, 8))
+    assert list(flags) == [2, 2]
+
+
 def test_empty_groups():
     """64 of the 256 digit-0 values never occur; the other groups still fit one tile over a chunk."""
     n = 512 * LINE_TILE
