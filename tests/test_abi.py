@@ -158,3 +158,16 @@ int main() {
            f"-L{PKG}", "-lrsort", f"-Wl,-rpath,{PKG}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("n,world", [(1 << 27, 8), (1 << 22, 2), (3 << 24, 4)])
+def test_multi_workspace_holds_any_local_sort(n, world):
+    """rsort_multi_workspace_size covers the local sort of any received count up to the capacity --
+    including counts whose plan is a digit-group plan with its joint-count rows (64 MiB) where the
+    capacity's own plan is not one: the partition buffer (4 n B) plus the largest sort workspace."""
+    lib = rs._lib()
+    cap = rs.default_capacity(n)
+    mw = int(lib.rsort_multi_workspace_size(n, cap, 8, 0, world))
+    sizes = {cap, cap // 2 + 1, n, 1 << 25, (1 << 24) + 5, 1 << 23, 3 << 22, 1 << 20, 1}
+    need = max(rs.workspace_size(m, 8) for m in sizes if m <= cap)
+    assert mw >= 4 * n + need, (mw, need)
