@@ -26,6 +26,7 @@
 #                    environment setting KV (e.g. RSORT_NX_TAIL=1), alternating twice
 #   wgt [args]       per-workgroup durations of each scatter pass, slowest chunks of pass 1 (dev/wgtimes_lab.py)
 #   sqzipf           SQ counters per pass of a Zipf-keys sort (LDS address / bank conflicts), in issue order
+#   pfloor           the pairs pass's write-stream floor (dev/ceiling_lab pairs) beside the pairs kernel, one box
 #   sqpmc            SQ counters (three passes) of a pairs pass (dev/pairs_lab) and a C3 sort (dev/sqpmc.py)
 #   prof TAG [args]  profiles/run_profiles.sh (kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes)
 #   pmc              memory-pipe PMC of rs_scatter_lines (dev/scatter_lab) vs the line-store lab (wc_lab)
@@ -322,6 +323,26 @@ ceiling)
     timeout -k 10 240 dev/ceiling_lab 30 10 > gpurun_out/ceiling.jsonl 2> gpurun_out/ceiling.err
     stop_unless_ok $? ceiling
     grep -v chunk_records gpurun_out/ceiling.jsonl | tail -n 30
+    ;;
+pfloor)
+    # the pairs pass's write-stream floor (dev/ceiling_lab pairs, built here) and, on the same box, the
+    # pairs kernel on uniform and Zipf pairs (bench.py, scatter ms per pass)
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 dev/ceiling_lab.hip -o /tmp/ceiling_lab_p || exit 1
+    timeout -k 10 120 /tmp/ceiling_lab_p 30 10 pairs > gpurun_out/pfloor.jsonl 2> gpurun_out/pfloor.err
+    stop_unless_ok $? pfloor
+    cat gpurun_out/pfloor.jsonl
+    for d in uniform zipf; do
+        timeout -k 10 200 python bench.py --dist $d --pairs --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
+            --configs "" > gpurun_out/pfloor_$d.json 2> gpurun_out/pfloor_$d.err
+        stop_unless_ok $? "pfloor $d"
+        python3 - "$d" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/pfloor_{sys.argv[1]}.json").read().strip().splitlines()[-1])
+r = d["roofline"]
+print("pairs %-8s %8.3f ms/sort  scatter %.4f ms/pass (%.3f)  %s" % (sys.argv[1], d["ms_per_step"], r["avg_launch_ms"],
+      r["frac"], d["verified"]))
+PY
+    done
     ;;
 wgtx)
     cp cuda.radixsort_amd/librsort.so gpurun_out/wgt_lib.so
