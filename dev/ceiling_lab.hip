@@ -156,6 +156,36 @@ __global__ __launch_bounds__(TH) void runs_pairs(const u32x4 *__restrict__ ink, 
     }
 }
 
+// runs64 variants that separate the two sides of the pairs stream's advantage: SPLITR reads each tile as
+// two halves from the two halves of the input (two read streams per workgroup, like keys + values);
+// SPLITW writes the odd digits' runs into a second array (two write arrays, like the pairs stream)
+template <int TH, int Q, bool SPLITR, bool SPLITW>
+__global__ __launch_bounds__(TH) void runs_split(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
+                                                 uint32_t *__restrict__ out2, uint64_t n, uint32_t tpc) {
+    constexpr uint32_t T = TH * Q * 4, L = T / 256;
+    const uint64_t region = n / 256 - 32;
+    const uint64_t half4 = n / 8;  // quads per input half
+    const uint64_t cbeg = (uint64_t)blockIdx.x * tpc * T;
+    for (uint32_t tile = 0; tile < tpc; ++tile) {
+        const uint64_t tb = cbeg + (uint64_t)tile * T;
+        if (tb + T > n) break;
+        u32x4 v[Q];
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            uint64_t qi = tb / 4 + threadIdx.x + j * TH;
+            if (SPLITR) qi = (j & 1) ? half4 + tb / 8 + threadIdx.x + (j / 2) * TH : tb / 8 + threadIdx.x + (j / 2) * TH;
+            v[j] = ld<true>(in + qi);
+        }
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const uint32_t i = (threadIdx.x + j * TH) * 4;
+            const uint32_t r = i / L;
+            const uint64_t pos = (SPLITW ? (r / 2) : r) * region + (uint64_t)blockIdx.x * tpc * L + (uint64_t)tile * L + (i % L);
+            st<true>(reinterpret_cast<u32x4 *>(((SPLITW && (r & 1)) ? out2 : out) + pos), v[j]);
+        }
+    }
+}
+
 static hipEvent_t e0, e1;
 static int g_reps = 10;
 
@@ -288,6 +318,43 @@ int main(int argc, char **argv) {
             const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
             double ms = timeit([&] { runs<TH, Q, true, true><<<g, TH>>>((const u32x4 *)a, b, n, tpc); });
             line("runs64", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+        }
+        {
+            constexpr int TH = 1024, Q = 4;
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            const u32x4 *A4 = (const u32x4 *)a;
+            double ms = timeit([&] { runs_split<TH, Q, true, false><<<g, TH>>>(A4, b, b2, n, tpc); });
+            line("runs64_splitread", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+            ms = timeit([&] { runs_split<TH, Q, false, true><<<g, TH>>>(A4, b, b2, n, tpc); });
+            line("runs64_splitwrite", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+            ms = timeit([&] { runs_split<TH, Q, true, true><<<g, TH>>>(A4, b, b2, n, tpc); });
+            line("runs64_splitboth", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+            ms = timeit([&] { runs_split<TH, Q, false, false><<<g, TH>>>(A4, b, b2, n, tpc); });
+            line("runs64_split_none", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+        }
+        {
+            // keys in 8192-key tiles: runs of 32 keys (128 B), as the pairs stream writes per array
+            constexpr int TH = 1024, Q = 2;
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            double ms = timeit([&] { runs<TH, Q, true, true><<<g, TH>>>((const u32x4 *)a, b, n, tpc); });
+            line("runs32", "chunk", TH, Q, 1, 1, 1, 8.0 * n, ms);
+        }
+        {
+            // pairs in 16384-pair tiles: runs of 64 pairs (256 B) per array
+            constexpr int TH = 1024, Q = 4;
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            const u32x4 *K = (const u32x4 *)a, *V = (const u32x4 *)a2;
+            double ms = timeit([&] { runs_pairs<TH, Q, true, true><<<g, TH>>>(K, V, b, b2, n, tpc); });
+            line("runs64_pairs", "chunk", TH, Q, 1, 1, 1, 16.0 * n, ms);
         }
         return 0;
     }
