@@ -292,10 +292,27 @@ int main(int argc, char **argv) {
         // `pairs`: the pairs pass's write-stream floor (8192-pair tiles, runs of 32 pairs in both arrays,
         // one chunk per CU) beside the keys pass's (runs64), 2^lg pairs: four 4 x 2^lg-B buffers
         uint32_t *a2, *b2;
-        CK(hipMalloc(&a2, nmax * 4));
-        CK(hipMalloc(&b2, nmax * 4));
-        CK(hipMemset(a2, 3, nmax * 4));
+        CK(hipMalloc(&a2, nmax * 4 + (4u << 20)));
+        CK(hipMalloc(&b2, nmax * 4 + (4u << 20)));
+        CK(hipMemset(a2, 3, nmax * 4 + (4u << 20)));
         const uint64_t n = nmax;
+        printf("{\"kind\": \"buffers\", \"a\": \"%p\", \"a2\": \"%p\", \"b\": \"%p\", \"b2\": \"%p\"}\n", (void *)a,
+               (void *)a2, (void *)b, (void *)b2);
+        {
+            // the values arrays moved by a few offsets (bytes): does the two-array floor depend on where the
+            // second array of each pair sits relative to the first?
+            constexpr int TH = 1024, Q = 2;
+            constexpr uint32_t T = TH * Q * 4;
+            const uint64_t tiles = n / T;
+            const uint32_t tpc = (uint32_t)((tiles + cus - 1) / cus);
+            const unsigned g = (unsigned)((tiles + tpc - 1) / tpc);
+            for (uint64_t off : {0ull, 1024ull, 4096ull, 65536ull + 256ull, 2097152ull + 4096ull}) {
+                const u32x4 *K = (const u32x4 *)a, *V = (const u32x4 *)(a2 + off / 4);
+                double ms = timeit([&] { runs_pairs<TH, Q, true, true><<<g, TH>>>(K, V, b, b2 + off / 4, n, tpc); });
+                printf("{\"kind\": \"runs32_pairs_off\", \"offset\": %llu, \"ms\": %.4f, \"TBs\": %.3f}\n",
+                       (unsigned long long)off, ms, 16.0 * n / ms / 1e9);
+            }
+        }
         {
             constexpr int TH = 1024, Q = 2;
             constexpr uint32_t T = TH * Q * 4;
