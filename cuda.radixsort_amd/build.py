@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = ["rsort_kernels.hip", "rsort_capi.cpp", "rsort_vendor.hip", "rsort_multi.cpp", "rsort_exchange.cpp"]
-HEADERS = [CSRC / "rsort_internal.hpp", ROOT / "include" / "rsort.h"]
+HEADERS = [CSRC / "rsort_internal.hpp", CSRC / "rsort_hooks.hpp", ROOT / "include" / "rsort.h"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=hidden",
           f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall"]
 

@@ -28,6 +28,7 @@ constexpr int kVersion = 100;  // 0.1.0
 std::atomic<int> g_rank_algo{RSORT_RANK_MATCH};
 std::atomic<int> g_group_chunks{1};
 std::atomic<int> g_table_fault{0};  // rsort_inject_table_fault (tests)
+std::atomic<int> g_rank_fault{0};   // rsort_inject_rank_fault (tests)
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -222,6 +223,7 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     ws += align256((size_t)p->table_entries * 4);            // chunk x digit table
     ws += align256((size_t)p->scan_blocks * 4);              // scan block sums
     ws += align256((size_t)(p->bins + 1) * 4);               // bucket starts (partition / top hist)
+    ws += 256;                                               // check words (tail-scan counter, check word)
     if (joint_plan(*p)) {
         ws += align256((size_t)kJointBins * kJointBins * 4 + 4);  // joint counts [next digit][digit], rows counter
         ws += align256((size_t)2 * kBoundsWords * 4);             // group bounds of passes 1 and 3
@@ -231,7 +233,6 @@ int plan_fill(int64_t n, int k, int pairs, int64_t tpc, rsort_plan *p, int parti
     }
     if (!partition && next_plan(*p)) {
         ws += align256((size_t)p->table_entries * 4);  // the next pass's table
-        ws += 256;                                     // the tail-scan counter / check words
         ws += align256((size_t)p->table_entries * 4);  // raw-table offsets: the third table of the rotation
     }
     p->workspace_bytes = ws;
@@ -268,6 +269,8 @@ Carve carve(const rsort_plan &p, void *ws) {
     q += align256((size_t)p.scan_blocks * 4);
     c.starts = (uint32_t *)q;
     q += align256((size_t)(p.bins + 1) * 4);
+    c.done = (uint32_t *)q;
+    q += 256;
     if (joint_plan(p)) {
         c.joint = (uint32_t *)q;
         c.rows_cnt = c.joint + kJointBins * kJointBins;  // (cleared with the joint counts)
@@ -284,8 +287,6 @@ Carve carve(const rsort_plan &p, void *ws) {
     if (next_plan(p)) {
         c.table2 = (uint32_t *)q;
         q += align256((size_t)p.table_entries * 4);
-        c.done = (uint32_t *)q;
-        q += 256;
         c.table3 = (uint32_t *)q;
     }
     return c;
@@ -300,8 +301,9 @@ Carve carve(const rsort_plan &p, void *ws) {
 // adds runs of equal pairs once (rs_histogram's run path), so pass 3 gets its own cut plan too.
 int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uint32_t *table,
                        uint32_t *joint, const uint32_t *enable, hipStream_t s, bool zero_joint,
-                       uint32_t *rows, uint32_t *rows_cnt) {
+                       uint32_t *rows, uint32_t *rows_cnt, uint32_t *done = nullptr) {
     HistArgs a{};
+    a.done = done;
     a.rows = rows;
     a.rows_cnt = rows_cnt;
     a.keys = keys;
@@ -406,8 +408,11 @@ int do_scatter(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, ui
                uint32_t *vout, int shift, const uint32_t *table, int local_only, int dmode,
                const uint32_t *split, int nsplit, hipStream_t s, const uint32_t *bounds = nullptr,
                uint32_t *next_table = nullptr, uint32_t *tail_zero = nullptr, uint32_t *done = nullptr,
-               const uint32_t *cl_select = nullptr, int raw_table = 0, uint32_t *zero_table = nullptr) {
+               const uint32_t *cl_select = nullptr, int raw_table = 0, uint32_t *zero_table = nullptr,
+               uint32_t *check = nullptr) {
     ScatterArgs a{};
+    a.check = check;
+    a.rank_fault = g_rank_fault.load() ? 1u : 0u;
     a.raw_table = raw_table ? 1u : 0u;
     a.zero_table = zero_table;
     a.cl_select = cl_select;
@@ -486,8 +491,6 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
     // next-digit counts (k = 3, 4): the same kernel conditions as digit groups
     const bool nextc = next_plan(p) && g_group_chunks.load() != 0 && internal_rank(g_rank_algo.load()) == kRankAtomic &&
                        line_capable(kout, nullptr, 0, p.n) && line_capable(c.tmp_k, nullptr, 0, p.n);
-    if (next_plan(p) && !nextc && hipMemsetAsync(c.done, 0, 8, s) != hipSuccess)  // rsort_plan_check: clean
-        return RSORT_ERR_HIP;
     // next-digit plans: every pass after the first derives its offsets from the raw counts the pass
     // before added (three tables in rotation: read / added into / cleared for the pass after next),
     // instead of the last workgroup of each pass scanning them (RSORT_NX_TAIL=1: that older way)
@@ -509,12 +512,14 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         uint32_t *nxt = (nextc && i + 1 < P) ? (rawt ? rot[(i + 1) % 3] : (i % 2 == 1) ? c.table : c.table2) : nullptr;
         uint32_t *clr = (rawt && i + 2 < P) ? rot[(i + 2) % 3] : nullptr;  // for the pass after next
         const uint32_t *enable = (count_joint && i >= 2) ? c.bounds + (i / 2 - 1) * kBoundsWords : nullptr;
+        // pass 0's histogram clears the check words (rsort_plan_check: a clean record for this sort)
         if (count_joint) {
-            if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable, s, i == 0, rows, rows_cnt)))
+            if ((st = do_histogram_joint(p, sk, shift, c.table, c.joint, enable, s, i == 0, rows, rows_cnt,
+                                         i == 0 ? c.done : nullptr)))
                 return st;
         } else if (!(nextc && i > 0) &&
                    (st = do_histogram(p, sk, shift, tab, kDigitShift, nullptr, 0, s, bounds, c.joint, c.plan,
-                                      c.pcounts, rawt ? nxt : nullptr, rawt ? c.done : nullptr,
+                                      c.pcounts, rawt ? nxt : nullptr, i == 0 ? c.done : nullptr,
                                       bounds ? rows : nullptr))) {
             return st;
         }
@@ -534,7 +539,7 @@ int sort_planned(const rsort_plan &p, const uint32_t *kin, const uint32_t *vin, 
         const uint32_t *cl = (joint && i >= 1) ? c.bounds + ((i - 1) / 2) * kBoundsWords : nullptr;
         if ((st = do_scatter(p, sk, sv, dk, dv, shift, tab, 0, kDigitShift, nullptr, 0, s, bounds, nxt,
                              (nxt && !rawt) ? tab : nullptr, (nextc && (nxt || rawt)) ? c.done : nullptr, cl,
-                             rawt, clr)))
+                             rawt, clr, c.done + kDoneErr)))
             return st;
         // test hook: corrupt the raw table pass 1 reads (its total is then not n: every pass-1 workgroup
         // writes nothing and records the failure for rsort_plan_check / RSORT_ERR_CHECK)
@@ -620,9 +625,9 @@ int host_sort(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t
         return RSORT_ERR_HIP;
     if (pairs && hipMemcpyAsync(vout, d_vout, (size_t)n * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return RSORT_ERR_HIP;
-    // this entry waits for the device anyway: the sort's self-check (rsort_plan_check) is read here
+    // this entry waits for the device anyway: the sort's self-checks (rsort_plan_check) are read here
     uint32_t check = 0;
-    if (next_plan(p) && hipMemcpyAsync(&check, carve(p, ws).done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (hipMemcpyAsync(&check, carve(p, ws).done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess)
         return RSORT_ERR_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
     return check ? RSORT_ERR_CHECK : RSORT_OK;
@@ -804,18 +809,20 @@ int rsort_plan_features(const rsort_plan *plan) {
 
 int rsort_inject_table_fault(int enable) { return g_table_fault.exchange(enable ? 1 : 0); }
 
+int rsort_inject_rank_fault(int enable) { return g_rank_fault.exchange(enable ? 1 : 0); }
+
 int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream) {
     if (!plan || !flags || !d_workspace) return RSORT_ERR_ARG;
     int st = check_plan(plan);
     if (st) return st;
     *flags = 0;
-    if (!next_plan(*plan) || plan->n == 0) return RSORT_OK;
+    if (plan->n == 0) return RSORT_OK;
     const Carve c = carve(*plan, const_cast<void *>(d_workspace));
     hipStream_t s = (hipStream_t)stream;
     uint32_t h = 0;
     if (hipMemcpyAsync(&h, c.done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return RSORT_ERR_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
-    *flags = h ? 1 : 0;
+    *flags = (int)(h & (kCheckTable | kCheckRankOrder));
     return RSORT_OK;
 }
 
@@ -906,10 +913,14 @@ int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
     if (workspace_bytes < p.workspace_bytes) return RSORT_ERR_WORKSPACE;
     const Carve c = carve(p, d_workspace);
     const int ns = num_buckets - 1;
-    if ((st = do_histogram(p, d_keys_in, 0, c.table, kDigitSplit, splitters, ns, s))) return st;
+    // (the check words as a sort's: cleared by the histogram, the scatter's rank check recorded there)
+    if ((st = do_histogram(p, d_keys_in, 0, c.table, kDigitSplit, splitters, ns, s, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, c.done)))
+        return st;
     if ((st = do_scan(p, c.table, c.bsums, s))) return st;
     if ((st = do_scatter(p, d_keys_in, d_vals_in, d_keys_out, d_vals_out, 0, c.table, 0, kDigitSplit,
-                         splitters, ns, s)))
+                         splitters, ns, s, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                         c.done + kDoneErr)))
         return st;
     return hip_status(launch_gather_starts(c.table, (uint32_t)p.num_chunks, (uint32_t)num_buckets,
                                            (uint64_t)n, d_bucket_starts, s));

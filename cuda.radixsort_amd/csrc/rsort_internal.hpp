@@ -139,6 +139,11 @@ struct ScatterArgs {
     // after next counts into)
     uint32_t raw_table;
     uint32_t *zero_table;
+    // the lane-ordered kernels (rs_scatter_lines, rs_scatter_pairs, rs_scatter with kRankAtomic): != nullptr ->
+    // the sort's check word (done + kDoneErr), where a workgroup whose per-tile rank check failed sets
+    // kCheckRankOrder; rank_fault != 0: the test hook that swaps two ranks per digit in every checked slot
+    uint32_t *check;
+    uint32_t rank_fault;
 };
 
 struct ScanArgs {
@@ -253,9 +258,12 @@ size_t scatter_kernels_used(char *buf, size_t len, int reset);
 // rsort_profile_*: while a thread's pause count is > 0 its launches record no phase events (the
 // multi-GPU sort's sample sort, which is part of its plan phase, not of the measured passes)
 void profile_pause(int delta);
-// Workspace check words (next-digit plans): done[kDoneErr] is set when a tail scan found a table
-// whose total is not n even after an agent-scope acquire and a second sweep.
+// Workspace check words (every plan: 256 B after the tables): done[0] is the tail-scan counter of next-digit
+// plans; done[kDoneErr] is the sort's check word, cleared by pass 0's histogram and read by rsort_plan_check /
+// the host entries. Its bits: kCheckTable -- a tail scan or a raw-table pass found a table whose total is not
+// n (next-digit plans); kCheckRankOrder -- a lane-ordered scatter kernel's per-tile rank check failed.
 constexpr uint32_t kDoneErr = 1;
+constexpr uint32_t kCheckTable = 1u, kCheckRankOrder = 2u;
 // Raw next-digit tables (every workgroup of a pass sums the whole R x C table for its own starts) cost
 // O(R x C) reads per workgroup, O(R x C^2) per pass: only plans of at most this many chunks (about one
 // resident wave: C2 has 1024) take them; larger ones keep the tail scan (DESIGN §8 measured

@@ -43,6 +43,7 @@
 #include <string>
 #include <vector>
 
+#include "rsort_hooks.hpp"
 #include "rsort_internal.hpp"
 
 namespace rsort {
@@ -178,16 +179,6 @@ __device__ __forceinline__ uint32_t rank_add_hot(uint32_t *cnt, uint32_t d, uint
     return atomicAdd(&cnt[d], 1u);
 }
 
-// slots per issue batch of the deferred ranking (0: rank_add / rank_add_hot slot by slot), per kernel
-#ifndef RSORT_DEFER_KEYS_CL
-#define RSORT_DEFER_KEYS_CL 2
-#endif
-#ifndef RSORT_DEFER_KEYS_PLAIN
-#define RSORT_DEFER_KEYS_PLAIN 0
-#endif
-#ifndef RSORT_DEFER_PAIRS
-#define RSORT_DEFER_PAIRS 4
-#endif
 // rank_add_hot in two halves, so a tile's KPT slots issue their returning adds back to back and
 // wait for the LDS once: hot_issue picks the slot's aggregated digit c (~0u: none) and its lanes m
 // exactly as rank_add_hot and issues the slot's one add; hot_rank, after every slot is issued, turns
@@ -304,6 +295,40 @@ __device__ __forceinline__ void peer_mask(uint32_t d, uint32_t &mlo, uint32_t &m
     }
 }
 
+// Per-tile check of the kRankAtomic premise (the reference checks every sort,
+// Parallel7.cu:679-687). The line and pairs kernels and rs_scatter run it on the first slot of a full tile
+// (every kRankCheckEvery-th tile of a chunk): each lane's rank r from the lane-ordered returning adds must
+// be base + (#lower lanes with its digit), with ONE base for all lanes of a digit. The lanes of a digit
+// come from BITS ballots (peer_mask), the base of the digit's first lane from one ds_bpermute. A change of
+// the lane order would permute the ranks among a digit's lanes -- the same keys in a wrong order, an
+// unstable sort that no checksum of the keys can see -- and duplicated ranks (lost keys) fail the same
+// test. Returns 1 where it failed. fault != 0 (test hook rsort_inject_rank_fault, ScatterArgs::rank_fault):
+// the first two lanes of every digit swap their ranks first, as a broken lane order would. ~40 VALU and
+// one bpermute per wave and checked tile; every lane of the wave must take part (full tiles only).
+template <int BITS>
+__device__ __forceinline__ uint32_t rank_check(uint32_t d, uint32_t &r, uint32_t fault) {
+    uint32_t mlo, mhi;
+    peer_mask<BITS>(d, mlo, mhi);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+    if (fault != 0u) {
+        const uint32_t peers = (uint32_t)__builtin_popcount(mlo) + (uint32_t)__builtin_popcount(mhi);
+        if (peers >= 2u && below < 2u) r = below == 0u ? r + 1u : r - 1u;
+    }
+    const uint32_t b = r - below;
+    const uint32_t first = mlo != 0u ? (uint32_t)__builtin_ctz(mlo) : 32u + (uint32_t)__builtin_ctz(mhi);
+    return (uint32_t)__shfl((int)b, (int)first) != b ? 1u : 0u;
+}
+
+// Tiles between rank checks in a chunk (a power of 2): the check on every tile cost C3 / C4 ~1 % (same-box
+// A/B); every 8th, starting with each chunk's first tile, checks 8-64 tiles per chunk and pass at C3 / C4.
+constexpr uint32_t kRankCheckEvery = 8;
+
+// End of a scatter workgroup: a wave any of whose lanes saw a failed rank_check sets kCheckRankOrder in the
+// sort's check word (rsort_plan_check; the host entries return RSORT_ERR_CHECK). Every lane must call it.
+__device__ __forceinline__ void report_order(uint32_t *check, uint32_t bad) {
+    if (check != nullptr && __ballot(bad != 0u) != 0ull && lane_id() == 0) atomicOr(check, kCheckRankOrder);
+}
+
 // Inclusive wave64 scan with DPP row shifts + row broadcasts (no LDS, no bpermute):
 // row_shr:1,2,4,8 scan each row of 16 lanes, row_bcast:15 / row_bcast:31 carry row totals.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -377,35 +402,6 @@ struct Digit {
     }
 };
 
-// Lab build (-DRSORT_WG_TIMES, dev/wgtimes_lab.py): every rs_scatter_lines workgroup (the first 2048 of a
-// pass; slot = shift / BITS) and every joint-count histogram workgroup (g_wg_htimes, slot = shift / 8)
-// records its start and end (s_memrealtime, 100 MHz) and its key range [beg, end), read back with
-// rsort_lab_wg_times; the upper halves of the range words hold where it ran: HW_ID (hwreg 4: cu 11:8,
-// sh 12, se 15:13) over beg, XCC_ID (hwreg 20) over end. Absent from the library.
-#ifdef RSORT_WG_TIMES
-__device__ unsigned long long g_wg_times[8][2048][4];
-__device__ unsigned long long g_wg_htimes[4][256][4];
-#define RS_WG_T0 const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();
-#define RS_WG_TREC(TAB, SLOT, NB, B, E)                                                           \
-    do {                                                                                          \
-        __syncthreads();                                                                          \
-        if (threadIdx.x == 0 && blockIdx.x < (NB)) {                                              \
-            unsigned long long *p_ = TAB[SLOT][blockIdx.x];                                       \
-            const unsigned long long hw_ = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   \
-            const unsigned long long xc_ = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  \
-            p_[0] = wg_t0_;                                                                       \
-            p_[1] = __builtin_amdgcn_s_memrealtime();                                             \
-            p_[2] = (unsigned long long)(B) | (hw_ << 32);                                        \
-            p_[3] = (unsigned long long)(E) | (xc_ << 32);                                        \
-        }                                                                                         \
-    } while (0)
-#define RS_WG_T1 RS_WG_TREC(g_wg_times, (a.shift / BITS) & 7u, 2048u, cbeg, cend)
-#define RS_WG_TH1 RS_WG_TREC(g_wg_htimes, (a.shift / 8u) & 3u, 256u, beg, end)
-#else
-#define RS_WG_T0
-#define RS_WG_T1
-#define RS_WG_TH1
-#endif
 // ------------------------------------------------------------------------------ histogram
 // Reference: histogramKernel (Parallel7.cu:318-343) + transpose (P7:361-392, :596).
 // SUB: each per-wave copy is split into SUB interleaved sub-counters (lane % SUB picks one), so
@@ -619,19 +615,20 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
         }
         return;
     }
+    // pass 0 of a sort (HistArgs::done): clear the check words on the way (before any scatter runs)
+    if (a.done != nullptr && blockIdx.x == 0 && t == 0) {
+        a.done[0] = 0u;
+        a.done[kDoneErr] = 0u;
+    }
     if constexpr (JOINT) {
         if (a.joint_enable == nullptr || *a.joint_enable != kGroupsFixed) {
             hist_joint_body<THREADS>(a, s_h, c, sub, S);
             return;
         }
     }
-    // raw-table plans (HistArgs::zero): clear the next table and the check words on the way
+    // raw-table plans (HistArgs::zero): clear the next table on the way
     for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < a.zero_n; i += (uint64_t)gridDim.x * THREADS)
         a.zero[i] = 0u;
-    if (a.done != nullptr && blockIdx.x == 0 && t == 0) {
-        a.done[0] = 0u;
-        a.done[kDoneErr] = 0u;
-    }
     for (uint32_t i = t; i < HW * R * SB; i += THREADS) s_h[i] = 0;
     __syncthreads();
 
@@ -986,7 +983,7 @@ __device__ void tail_scan(uint32_t *table, uint64_t m, uint32_t *zero, uint32_t 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __syncthreads();  // every wave has read s_ws before it is written again
     }
-    if (total != expect && t == 0) atomicOr(&done[kDoneErr], 1u);
+    if (total != expect && t == 0) atomicOr(&done[kDoneErr], kCheckTable);
     u32x4 *q = reinterpret_cast<u32x4 *>(table);
     for (uint32_t b0 = qb; b0 < qe; b0 += B * kWave) {
         u32x4 v[B];
@@ -1433,8 +1430,11 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
+    uint32_t order_bad = 0;  // kRankAtomic: the per-tile rank check (rank_check) failed in this thread
 
-    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+    for (uint64_t tb = cbeg, tno = 0; tb < cend; tb += T, ++tno) {
+        // the rank check on every kRankCheckEvery-th tile of a chunk, its first included (workgroup-uniform)
+        const bool check_tile = (tno & (kRankCheckEvery - 1)) == 0;
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
         // tl: the thread index made opaque per tile, so LICM cannot hoist the KPT output
         // positions tl + j*THREADS out of the loop into KPT live registers; output slot j of
@@ -1501,7 +1501,8 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
                     // that hit the same address in ascending lane order, so lane l receives
                     // base + (#lower lanes with its digit) -- the stable rank, with no ballots
                     // (rank_add; the library probes this once per device, rs_lane_order_probe)
-                    const uint32_t p = rank_add(&s_cnt[w * R], d);
+                    uint32_t p = rank_add(&s_cnt[w * R], d);
+                    if (j == 0 && valid == T && check_tile) order_bad |= rank_check<BITS>(d, p, a.rank_fault);
                     s_keys[p] = key[j];
                     if constexpr (PAIRS) s_vals[p] = val[j];
                     continue;
@@ -1620,6 +1621,7 @@ __global__ __launch_bounds__(THREADS, MINW > 0 ? MINW : 1) void rs_scatter(Scatt
             if (nb < cend) load_tile(nb, key, val);
         }
     }
+    if constexpr (RANK == kRankAtomic) report_order(a.check, order_bad);
 }
 
 // ------------------------------------------------------------------------------ raw-table offsets
@@ -1684,7 +1686,7 @@ __device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint6
 #pragma unroll
         for (uint32_t i = 0; i < R; ++i) pre += i < t ? s_tot[i] : 0u;
         s_base[t] += pre;
-        if (c == 0 && t == 0 && tot != n && err != nullptr) err[0] = 1u;
+        if (c == 0 && t == 0 && tot != n && err != nullptr) atomicOr(err, kCheckTable);
     }
     __syncthreads();
     return tot == n;
@@ -1715,14 +1717,8 @@ __device__ bool raw_offsets(const uint32_t *table, uint32_t C, uint32_t c, uint6
 // remaining carries are flushed with masked dword stores (both lines are shared with the
 // neighbouring chunks' output). Only the grid's very last tile is partial (chunks are whole
 // tiles), so the full-tile paths carry no per-slot predicates.
-#ifndef RSORT_LINES_MINW_SMALL
-#define RSORT_LINES_MINW_SMALL 1
-#endif
-#ifndef RSORT_NXR
-#define RSORT_NXR 8
-#endif
 template <int BITS, int THREADS, int KPT, int G, bool PAIRS, int DMODE, int NT = 0, int CL = 0>
-__global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 1) void rs_scatter_lines(ScatterArgs a) {
+__global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmall : 1) void rs_scatter_lines(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;
@@ -1755,7 +1751,7 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     // share (digit, slot) -- a digit's lines are adjacent -- so without them ~4 lanes would hit
     // each of the R counters and serialise in the LDS
     constexpr bool NX = (R <= 16) && DMODE == kDigitShift;
-    constexpr uint32_t NXR = RSORT_NXR;
+    constexpr uint32_t NXR = hooks::kNextReplicas;
     __shared__ uint32_t s_next[NX ? 2 * R * R * NXR : 1];
     __shared__ uint32_t s_nb[NX ? R : 1];  // first position of digit d's second output chunk
     __shared__ uint32_t s_oc[NX ? R : 1];  // digit d's first output chunk
@@ -1881,19 +1877,19 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         }
         if (lo <= q) {
             if constexpr ((NT & 2) != 0) {  // non-temporal whole-line stores
-                __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
-                if constexpr (PAIRS) __builtin_nontemporal_store(vv, reinterpret_cast<u32x4 *>(a.vout + gp));
+                hooks::store_quad_nt(a.kout + gp, kv);
+                if constexpr (PAIRS) hooks::store_quad_nt(a.vout + gp, vv);
             } else {
-                *reinterpret_cast<u32x4 *>(a.kout + gp) = kv;
-                if constexpr (PAIRS) *reinterpret_cast<u32x4 *>(a.vout + gp) = vv;
+                hooks::store_quad(a.kout + gp, kv);
+                if constexpr (PAIRS) hooks::store_quad(a.vout + gp, vv);
             }
         } else {
             // the chunk's first line: lanes below lo belong to the previous chunk
 #pragma unroll
             for (uint32_t x = 0; x < 4; ++x)
                 if (lo <= q + x) {
-                    a.kout[gp + x] = kv[x];
-                    if constexpr (PAIRS) a.vout[gp + x] = vv[x];
+                    hooks::store_word(a.kout + gp + x, kv[x]);
+                    if constexpr (PAIRS) hooks::store_word(a.vout + gp + x, vv[x]);
                 }
         }
     };
@@ -1920,8 +1916,11 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
     };
 
     uint32_t hotd = 0xFFFFFFFFu;  // CL: the wave's last aggregated digit (none yet)
+    uint32_t order_bad = 0;       // the per-tile rank check (rank_check) failed in this thread
 
-    for (uint64_t tb = cbeg; tb < cend; tb += T) {
+    for (uint64_t tb = cbeg, tno = 0; tb < cend; tb += T, ++tno) {
+        // the rank check on every kRankCheckEvery-th tile of a chunk, its first included (workgroup-uniform)
+        const bool check_tile = (tno & (kRankCheckEvery - 1)) == 0;
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
         const bool full = valid == T && head == 0;
         const uint64_t nb = tb + T;
@@ -1943,7 +1942,7 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
         for (int i = 0; i < (PD ? (KPT + 7) / 8 : 1); ++i) dpk[i] = 0;
         uint32_t nkey[KPT];
         uint32_t nval[PAIRS ? KPT : 1];
-        constexpr int DB = CL ? RSORT_DEFER_KEYS_CL : RSORT_DEFER_KEYS_PLAIN;
+        constexpr int DB = CL ? hooks::kDeferKeysCl : hooks::kDeferKeysPlain;
         if (full && DB > 0 && !PD) {
             // deferred ranking: batches of DB slots issue their adds, then turn the returns into ranks
             static_assert(DB == 0 || KPT % (DB > 0 ? DB : 1) == 0, "whole batches");
@@ -1957,7 +1956,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
 #pragma unroll
                 for (int u = 0; u < DB; ++u) {
                     const int j = j0 + u;
-                    const uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
+                    uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
+                    if (j == 0 && check_tile) order_bad |= rank_check<BITS>(dig(key[j]), r, a.rank_fault);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
@@ -1968,7 +1968,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
                 // on uniform keys, 1.7x on clustered ones; dev/lines_exp.hip "rank1" +4% uniform)
                 const uint32_t dj = dig(key[j]);
                 if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
-                const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                if (j == 0 && check_tile) order_bad |= rank_check<BITS>(dj, r, a.rank_fault);
                 rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
         } else {
@@ -2133,8 +2134,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
             const uint32_t x = item % G;
             if ((fl.y & 0xFFu) <= x && x < (fl.y >> 8)) {
                 const uint32_t k = s_stage[CAP + item];
-                a.kout[(uint64_t)fl.x + x] = k;
-                if constexpr (PAIRS) a.vout[(uint64_t)fl.x + x] = s_vstage[CAP + item];
+                hooks::store_word(a.kout + (uint64_t)fl.x + x, k);
+                if constexpr (PAIRS) hooks::store_word(a.vout + (uint64_t)fl.x + x, s_vstage[CAP + item]);
                 if constexpr (NX) {
                     const uint32_t d = item / G;
                     if (count_next) next_add(d, fl.x + x - a.pos_shift >= s_nb[d] ? 1u : 0u, k);
@@ -2163,29 +2164,10 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
             }
         }
     }
+    report_order(a.check, order_bad);
     RS_WG_T1;
 }
 
-// Lab builds (-DRSORT_STAMPS, dev/pairs_lab.hip): per-phase s_memtime cycle totals of thread 0 into
-// ScatterArgs::stamps[workgroup * 8 + phase]. Empty in the library.
-#ifdef RSORT_STAMPS
-#define RS_STAMP_DECL unsigned long long st_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev_ = __builtin_amdgcn_s_memtime();
-#define RS_STAMP(i)                                                   \
-    do {                                                              \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-        st_acc_[i] += now_ - st_prev_;                                \
-        st_prev_ = now_;                                              \
-    } while (0)
-#define RS_STAMP_FLUSH()                                                                   \
-    do {                                                                                   \
-        if (threadIdx.x == 0 && a.stamps)                                                  \
-            for (int i_ = 0; i_ < 8; ++i_) a.stamps[blockIdx.x * 8 + i_] = st_acc_[i_];    \
-    } while (0)
-#else
-#define RS_STAMP_DECL
-#define RS_STAMP(i)
-#define RS_STAMP_FLUSH()
-#endif
 
 // ------------------------------------------------------------------------------ scatter (pairs, 128-B lines)
 // rs_scatter_pairs: the pass of rs_scatter_lines for key + value pairs with whole 128-B lines in BOTH
@@ -2211,15 +2193,10 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? RSORT_LINES_MINW_SMALL : 
 // A chunk starts with `inv` invalid leading slots per digit (its first line begins before the
 // chunk's output) and ends with masked dword stores of the carries (both lines are shared with the
 // neighbouring chunks). Digit-group chunks (a.bounds) and the clustered-input ranking (CL) as in
-// rs_scatter_lines.
-// (lab knobs, dev/pairs_lab.hip: PF = 2 tiles of loads in flight; OPT & 1 non-temporal loads, OPT & 2
-// the next tile's loads issued before the rank loop instead of after it, OPT & 4 keys and values
-// staged interleaved, OPT & 8 step 4 deferred to after the next tile's rank phase,
-// OPT & 16 / 32 the next tile's loads issued after step 2 / step 3 instead of after the rank phase,
-// OPT & 64 keys and values through ONE staging array in turn: steps 3 and 4 for the keys, then for the
-// values at the same slots (kept in registers) -- half the LDS, so two workgroups fit per CU)
-template <int BITS, int THREADS, int KPT, int CL = 0, int PF = 1, int OPT = 0>
-__global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) void rs_scatter_pairs(ScatterArgs a) {
+// rs_scatter_lines. (The measured variants of this kernel -- two tiles of loads in flight, interleaved or
+// sequential staging, deferred output, other load points -- are dev/pairs_variants.hpp.)
+template <int BITS, int THREADS, int KPT, int CL = 0>
+__global__ __launch_bounds__(THREADS, 1) void rs_scatter_pairs(ScatterArgs a) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int W = THREADS / kWave;
     constexpr int SEG = kWave * KPT;
@@ -2236,14 +2213,8 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
     static_assert(CAP + 40 < 65536u && NLM < 65536u, "slot and line indices packed in 16 bits");
 
     // [0, CAP) segments; [CAP, CAP + 32) the last tail read's overrun; CAP + 32 the padding sink
-    // OPT & 4: one interleaved {key, value} array (8-B stores per pair) instead of two
-    constexpr bool IL = (OPT & 4) != 0;
-    constexpr bool DEFER = (OPT & 8) != 0;
-    constexpr bool SQ = (OPT & 64) != 0;
-    static_assert(!(SQ && (IL || DEFER)), "sequential staging: two plain arrays' worth of work in one");
-    __shared__ __attribute__((aligned(16))) uint32_t s_k[IL ? 4 : CAP + 36];
-    __shared__ __attribute__((aligned(16))) uint32_t s_v[(IL || SQ) ? 4 : CAP + 36];
-    __shared__ __attribute__((aligned(16))) uint2 s_kv[IL ? CAP + 36 : 2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[CAP + 36];
+    __shared__ __attribute__((aligned(16))) uint32_t s_v[CAP + 36];
     constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
     __shared__ uint32_t s_cnt[W * RS + 1];
     __shared__ uint4 s_rec[R];        // per digit: {global - 32 x first line, LDS - 32 x first line, first line << 8 | inv}
@@ -2294,8 +2265,8 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
         if (valid == T) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                k[j] = (OPT & 1) ? __builtin_nontemporal_load(tk + j * kWave) : tk[j * kWave];
-                v[j] = (OPT & 1) ? __builtin_nontemporal_load(tv + j * kWave) : tv[j * kWave];
+                k[j] = tk[j * kWave];
+                v[j] = tv[j * kWave];
             }
         } else {
             const uint32_t lim = valid > lb ? valid - lb : 0u;
@@ -2319,68 +2290,26 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
         const uint32_t V = item / QPL, q = (item % QPL) * 4u;
         const uint2 lr = s_lrec[V];
         const uint32_t li = (lr.y & 0xFFFFu) + q;
-        u32x4 kv, vv;
-        if constexpr (IL) {
-            const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[li]);
-            const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[li + 2]);
-            kv = u32x4{p01.x, p01.z, p23.x, p23.z};
-            vv = u32x4{p01.y, p01.w, p23.y, p23.w};
-        } else {
-            kv = *reinterpret_cast<const u32x4 *>(&s_k[li]);
-            vv = *reinterpret_cast<const u32x4 *>(&s_v[li]);
-        }
+        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_k[li]);
+        const u32x4 vv = *reinterpret_cast<const u32x4 *>(&s_v[li]);
         const uint64_t gp = (uint64_t)(lr.x + q);
         const uint32_t lo = lr.y >> 16;
         if (lo <= q) {
-            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(a.kout + gp));
-            __builtin_nontemporal_store(vv, reinterpret_cast<u32x4 *>(a.vout + gp));
+            hooks::store_quad_nt(a.kout + gp, kv);
+            hooks::store_quad_nt(a.vout + gp, vv);
         } else {
             // the chunk's first line of this digit: lanes below lo belong to the previous chunk
 #pragma unroll
             for (uint32_t x = 0; x < 4; ++x)
                 if (lo <= q + x) {
-                    a.kout[gp + x] = kv[x];
-                    a.vout[gp + x] = vv[x];
+                    hooks::store_word(a.kout + gp + x, kv[x]);
+                    hooks::store_word(a.vout + gp + x, vv[x]);
                 }
         }
     };
 
-    // SQ: one array's quad of whole line item / QPL from the staging array (the keys' or the values')
-    auto store_one = [&](uint32_t item, uint32_t *__restrict__ dst) {
-        const uint32_t V = item / QPL, q = (item % QPL) * 4u;
-        const uint2 lr = s_lrec[V];
-        const u32x4 kv = *reinterpret_cast<const u32x4 *>(&s_k[(lr.y & 0xFFFFu) + q]);
-        const uint64_t gp = (uint64_t)(lr.x + q);
-        const uint32_t lo = lr.y >> 16;
-        if (lo <= q) {
-            __builtin_nontemporal_store(kv, reinterpret_cast<u32x4 *>(dst + gp));
-        } else {
-#pragma unroll
-            for (uint32_t x = 0; x < 4; ++x)
-                if (lo <= q + x) dst[gp + x] = kv[x];
-        }
-    };
-    // SQ: one array's tails (from the staging array) into its carry registers, and its whole lines out
-    auto output_one = [&](const uint32_t S, const uint32_t wl, const uint32_t pending, const uint32_t nlines,
-                          uint32_t (&cr)[CPT], uint32_t *__restrict__ dst) {
-        const uint32_t tl0 = S + wl * G + sub * CPT;
-        const uint32_t ncarry = pending - wl * G;
-#pragma unroll
-        for (uint32_t i = 0; i < CPT; i += 4) {
-            if (sub * CPT + i >= ncarry) break;
-            const u32x4 q4 = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
-            cr[i] = q4.x; cr[i + 1] = q4.y; cr[i + 2] = q4.z; cr[i + 3] = q4.w;
-        }
-        const uint32_t nq = nlines * QPL;
-        for (uint32_t item = t; item < nq; item += 2 * THREADS) {
-            store_one(item, dst);
-            if (item + THREADS < nq) store_one(item + THREADS, dst);
-        }
-    };
-
     RS_STAMP_DECL
-    // ---- 4. (of a tile) the tails back into the carry registers (the quads holding any); whole lines
-    //      out. DEFER: run after the NEXT tile's rank phase instead of at the end of the tile.
+    // ---- 4. (of a tile) the tails back into the carry registers (the quads holding any); whole lines out
     auto output = [&](const uint32_t S, const uint32_t wl, const uint32_t pending, const uint32_t nlines,
                       const uint32_t cnt) {
         {
@@ -2389,16 +2318,8 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
 #pragma unroll
             for (uint32_t i = 0; i < CPT; i += 4) {
                 if (sub * CPT + i >= ncarry) break;
-                u32x4 kq, vq;
-                if constexpr (IL) {
-                    const u32x4 p01 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i]);
-                    const u32x4 p23 = *reinterpret_cast<const u32x4 *>(&s_kv[tl0 + i + 2]);
-                    kq = u32x4{p01.x, p01.z, p23.x, p23.z};
-                    vq = u32x4{p01.y, p01.w, p23.y, p23.w};
-                } else {
-                    kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
-                    vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
-                }
+                const u32x4 kq = *reinterpret_cast<const u32x4 *>(&s_k[tl0 + i]);
+                const u32x4 vq = *reinterpret_cast<const u32x4 *>(&s_v[tl0 + i]);
                 ck[i] = kq.x; ck[i + 1] = kq.y; ck[i + 2] = kq.z; ck[i + 3] = kq.w;
                 cv[i] = vq.x; cv[i + 1] = vq.y; cv[i + 2] = vq.z; cv[i + 3] = vq.w;
             }
@@ -2413,241 +2334,166 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
         carry = pending - wl * G;
         g_run += cnt;
     };
-    uint32_t pS = 0, pwl = 0, ppend = 0, pnl = 0, pcnt = 0;  // DEFER: the staged tile's step-4 state
-    bool have_prev = false;
 
-    // The tile step. PF = 1: the next tile's loads go into nkey at the end of the rank phase and
-    // move into key at the end of the step. PF = 2: two register sets alternate (the loop is unrolled
-    // by two); a tile's set takes the loads of the tile two ahead as soon as it is staged.
     uint32_t hotd = 0xFFFFFFFFu;
-    auto tile_step = [&](const uint64_t tb, uint32_t (&key)[KPT], uint32_t (&val)[KPT]) {
-            const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
-            const bool full = valid == T && head == 0;
-            const uint64_t nb = tb + T;
-            uint32_t plim = valid > base ? valid - base : 0u;
-            asm volatile("" : "+v"(plim));
-            const bool h0 = base >= head;
-            head = 0;
-            // ---- 1. per-wave digit histogram; the returning add is the key's rank among its wave's
-            //      keys of that digit (lane order, kRankAtomic); two ranks per register
-    #pragma unroll
-            for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
-            uint32_t rk[(KPT + 1) / 2];
-            uint32_t nkey[PF == 1 ? KPT : 1], nval[PF == 1 ? KPT : 1];
-            if constexpr (PF == 1 && (OPT & 2)) {
-                if (nb < cend) load_tile(nb, nkey, nval);
-            }
-            constexpr int DB = RSORT_DEFER_PAIRS;
-            if (full && DB > 0) {
-                // deferred ranking (hot_issue / hot_rank): the slots' adds back to back, one LDS wait
-                // per batch of DB slots (C4: 3.45 vs 3.48 ms per pass, dev/lab.sh ab)
-                static_assert(DB == 0 || KPT % (DB > 0 ? DB : 1) == 0, "whole batches");
-    #pragma unroll
-                for (int j0 = 0; j0 < KPT; j0 += (DB > 0 ? DB : 1)) {
-                    uint32_t o[DB > 0 ? DB : 1], cc[DB > 0 ? DB : 1];
-                    uint64_t mm[DB > 0 ? DB : 1];
-    #pragma unroll
-                    for (int u = 0; u < DB; ++u)
-                        o[u] = hot_issue<CL != 0>(&s_cnt[w * RS], dig(key[j0 + u]), hotd, cc[u], mm[u]);
-    #pragma unroll
-                    for (int u = 0; u < DB; ++u) {
-                        const int j = j0 + u;
-                        const uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
-                        rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
-                    }
-                }
-            } else if (full) {
-    #pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t dj = dig(key[j]);
-                    const uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
-                    rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
-                }
-            } else {
-    #pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t d = dig(key[j]);
-                    uint32_t r = 0;
-                    if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
+    uint32_t order_bad = 0;  // the per-tile rank check (rank_check) failed in this thread
+    uint32_t key[KPT], val[KPT];
+    if (cbeg < cend) load_tile(cbeg, key, val);
+    for (uint64_t tb = cbeg, tno = 0; tb < cend; tb += T, ++tno) {
+        // the rank check on every kRankCheckEvery-th tile of a chunk, its first included (workgroup-uniform)
+        const bool check_tile = (tno & (kRankCheckEvery - 1)) == 0;
+        const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
+        const bool full = valid == T && head == 0;
+        const uint64_t nb = tb + T;
+        uint32_t plim = valid > base ? valid - base : 0u;
+        asm volatile("" : "+v"(plim));
+        const bool h0 = base >= head;
+        head = 0;
+        // ---- 1. per-wave digit histogram; the returning add is the key's rank among its wave's
+        //      keys of that digit (lane order, kRankAtomic); two ranks per register
+#pragma unroll
+        for (uint32_t i = lane; i < R; i += kWave) s_cnt[w * RS + i] = 0;
+        uint32_t rk[(KPT + 1) / 2];
+        uint32_t nkey[KPT], nval[KPT];
+        constexpr int DB = hooks::kDeferPairs;
+        if (full && DB > 0) {
+            // deferred ranking (hot_issue / hot_rank): the slots' adds back to back, one LDS wait
+            // per batch of DB slots (C4: 3.45 vs 3.48 ms per pass, dev/lab.sh ab)
+            static_assert(DB == 0 || KPT % (DB > 0 ? DB : 1) == 0, "whole batches");
+#pragma unroll
+            for (int j0 = 0; j0 < KPT; j0 += (DB > 0 ? DB : 1)) {
+                uint32_t o[DB > 0 ? DB : 1], cc[DB > 0 ? DB : 1];
+                uint64_t mm[DB > 0 ? DB : 1];
+#pragma unroll
+                for (int u = 0; u < DB; ++u)
+                    o[u] = hot_issue<CL != 0>(&s_cnt[w * RS], dig(key[j0 + u]), hotd, cc[u], mm[u]);
+#pragma unroll
+                for (int u = 0; u < DB; ++u) {
+                    const int j = j0 + u;
+                    uint32_t r = hot_rank(o[u], dig(key[j]), cc[u], mm[u]);
+                    if (j == 0 && check_tile) order_bad |= rank_check<BITS>(dig(key[j]), r, a.rank_fault);
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
-            RS_STAMP(5);
-            if constexpr (PF == 1 && !(OPT & (2 | 16 | 32))) {
-                if (nb < cend) load_tile(nb, nkey, nval);
+        } else if (full) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t dj = dig(key[j]);
+                uint32_t r = CL ? rank_add_hot(&s_cnt[w * RS], dj, hotd) : rank_add(&s_cnt[w * RS], dj);
+                if (j == 0 && check_tile) order_bad |= rank_check<BITS>(dj, r, a.rank_fault);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
-            if constexpr (DEFER) {
-                // the previous tile's output: its stores then have steps 2-3 of this tile to drain
-                // before the next vmcnt wait (at the next rank phase), instead of none
-                if (have_prev) output(pS, pwl, ppend, pnl, pcnt);
-                have_prev = true;
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = dig(key[j]);
+                uint32_t r = 0;
+                if ((uint32_t)(j * kWave) < plim && (j != 0 || h0)) r = atomicAdd(&s_cnt[w * RS + d], 1u);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
             }
-            // (the previous tile's step 4 has read the bitmap, records and staging area: behind the
-            // barrier below)
-            __syncthreads();
-            RS_STAMP(0);
-
-            // ---- 2. segments, bases, carry in, line marks
-            constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
-            uint32_t part = 0;
-            uint32_t wx[WPT];
-            if (sub < (uint32_t)W) {
-    #pragma unroll
-                for (uint32_t i = 0; i < WPT; ++i) {
-                    const uint32_t v = sub * WPT + i;
-                    wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
-                    part += wx[i];
-                }
-            }
-            uint32_t gpre, cnt;
-            group_scan<TPD>(part, sub, gpre, cnt);
-            // (carry, g_run, inv are the same in every thread of the group)
-            const uint32_t A = g_run - carry;          // line-aligned
-            const uint32_t pending = carry + cnt;      // slots from A on
-            const uint32_t wl = pending / G;           // whole lines written this tile
-            const uint32_t seg = (pending + 3u) & ~3u;
-            if (t < NBW) s_bits[t] = 0u;
-            uint32_t tot;
-            const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
-            RS_STAMP(7);
-            const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
-            const uint32_t nlines = tot >> 16;
-            if (sub < (uint32_t)W) {
-                uint32_t acc = S + carry + gpre;
-    #pragma unroll
-                for (uint32_t i = 0; i < WPT; ++i) {
-                    const uint32_t v = sub * WPT + i;
-                    if (v < (uint32_t)W) s_cnt[v * RS + d_own] = acc;
-                    acc += wx[i];
-                }
-            }
-            // the carry from registers into the segment head, whole quads (a quad past the carry's end
-            // lies inside the segment and is overwritten by step 3)
-    #pragma unroll
-            for (uint32_t i = 0; i < CPT; i += 4) {
-                if (sub * CPT + i < carry) {
-                    if constexpr (IL) {
-                        *reinterpret_cast<u32x4 *>(&s_kv[S + sub * CPT + i]) = u32x4{ck[i], cv[i], ck[i + 1], cv[i + 1]};
-                        *reinterpret_cast<u32x4 *>(&s_kv[S + sub * CPT + i + 2]) =
-                            u32x4{ck[i + 2], cv[i + 2], ck[i + 3], cv[i + 3]};
-                    } else {
-                        *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
-                        if constexpr (!SQ)
-                            *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
-                    }
-                }
-            }
-            if (leader) {
-                s_rec[d_own] = make_uint4(A - LS * G, S - LS * G, (LS << 8) | inv, 0u);
-                if (wl > 0) {
-                    s_mark[LS] = (uint8_t)d_own;
-                    atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
-                }
-            }
-            RS_STAMP(6);
-            __syncthreads();
-            RS_STAMP(1);
-            if constexpr (PF == 1 && (OPT & 16)) {
-                if (nb < cend) load_tile(nb, nkey, nval);
-            }
-
-            // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
-            //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
-            //      (batches of 8: all reads before the stores)
-            for (uint32_t V = t; V < nlines; V += THREADS) {
-                const uint4 rec = s_rec[line_digit(V)];
-                const uint32_t lo = (rec.z >> 8) == V ? (rec.z & 0xFFu) : 0u;
-                s_lrec[V] = make_uint2(rec.x + V * G, (rec.y + V * G) | (lo << 16));
-            }
-            RS_STAMP(2);
-            constexpr int SB = KPT < 8 ? KPT : 8;
-            static_assert(KPT % SB == 0, "whole batches of slots");
-            uint32_t sidx[SQ ? KPT : 1];  // SQ: every slot's staging index, for the values after the keys
-    #pragma unroll
-            for (int j0 = 0; j0 < KPT; j0 += SB) {
-                uint32_t pp[SB];
-    #pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int j = j0 + u;
-                    asm volatile("" : "+v"(key[j]));
-                    pp[u] = s_cnt[w * RS + dig(key[j])] + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-    #pragma unroll
-                for (int u = 0; u < SB; ++u) {
-                    const int j = j0 + u;
-                    uint32_t idx = pp[u];
-                    if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
-                    if constexpr (IL) {
-                        s_kv[idx] = make_uint2(key[j], val[j]);
-                    } else if constexpr (SQ) {
-                        s_k[idx] = key[j];
-                        sidx[j] = idx;
-                    } else {
-                        s_k[idx] = key[j];
-                        s_v[idx] = val[j];
-                    }
-                }
-            }
-            // PF = 2: this tile's registers are free (staged): the tile after next goes into them, in
-            // flight through this tile's output and the whole next tile
-            if constexpr (PF == 2) {
-                if (nb + T < cend) load_tile(nb + T, key, val);
-            }
-            __syncthreads();
-            RS_STAMP(3);
-            if constexpr (PF == 1 && (OPT & 32)) {
-                if (nb < cend) load_tile(nb, nkey, nval);
-            }
-
-            if constexpr (SQ) {
-                // the keys' lines and tails; then the values through the same slots: their carry into the
-                // segment heads, staged at the keys' indices, their lines and tails
-                output_one(S, wl, pending, nlines, ck, a.kout);
-                __syncthreads();
-                // (dword by dword: no barrier separates these from the staging below, so a whole quad
-                // past the carry's end could land after a staged value)
-    #pragma unroll
-                for (uint32_t i = 0; i < CPT; ++i)
-                    if (sub * CPT + i < carry) s_k[S + sub * CPT + i] = cv[i];
-    #pragma unroll
-                for (int j = 0; j < KPT; ++j) s_k[sidx[j]] = val[j];
-                __syncthreads();
-                output_one(S, wl, pending, nlines, cv, a.vout);
-                if (wl > 0) inv = 0;
-                carry = pending - wl * G;
-                g_run += cnt;
-            } else if constexpr (DEFER) {
-                pS = S;
-                pwl = wl;
-                ppend = pending;
-                pnl = nlines;
-                pcnt = cnt;
-            } else {
-                output(S, wl, pending, nlines, cnt);
-            }
-            if constexpr (PF == 1) {
-    #pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    key[j] = nkey[j];
-                    val[j] = nval[j];
-                }
-            }
-    };
-    uint32_t keyA[KPT], valA[KPT];
-    if (cbeg < cend) load_tile(cbeg, keyA, valA);
-    if constexpr (PF == 1) {
-        for (uint64_t tb = cbeg; tb < cend; tb += T) tile_step(tb, keyA, valA);
-    } else {
-        uint32_t keyB[KPT], valB[KPT];
-        if (cbeg + T < cend) load_tile(cbeg + T, keyB, valB);
-        for (uint64_t tb = cbeg; tb < cend; tb += 2 * T) {
-            tile_step(tb, keyA, valA);
-            if (tb + T < cend) tile_step(tb + T, keyB, valB);
         }
-    }
-    if constexpr (DEFER) {
-        if (have_prev) output(pS, pwl, ppend, pnl, pcnt);
+        RS_STAMP(5);
+        // the next tile's loads: in flight through steps 2-4 (issued earlier or later measured slower,
+        // dev/pairs_variants.hpp)
+        if (nb < cend) load_tile(nb, nkey, nval);
+        // (the previous tile's step 4 has read the bitmap, records and staging area: behind the
+        // barrier below)
+        __syncthreads();
+        RS_STAMP(0);
+
+        // ---- 2. segments, bases, carry in, line marks
+        constexpr uint32_t WPT = (W >= (int)TPD) ? W / TPD : 1;
+        uint32_t part = 0;
+        uint32_t wx[WPT];
+        if (sub < (uint32_t)W) {
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                wx[i] = v < (uint32_t)W ? s_cnt[v * RS + d_own] : 0u;
+                part += wx[i];
+            }
+        }
+        uint32_t gpre, cnt;
+        group_scan<TPD>(part, sub, gpre, cnt);
+        // (carry, g_run, inv are the same in every thread of the group)
+        const uint32_t A = g_run - carry;          // line-aligned
+        const uint32_t pending = carry + cnt;      // slots from A on
+        const uint32_t wl = pending / G;           // whole lines written this tile
+        const uint32_t seg = (pending + 3u) & ~3u;
+        if (t < NBW) s_bits[t] = 0u;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan1<THREADS>(leader ? (seg | (wl << 16)) : 0u, s_ws, tot);
+        RS_STAMP(7);
+        const uint32_t S = group_lane<TPD>(pre, 0) & 0xFFFFu, LS = group_lane<TPD>(pre, 0) >> 16;
+        const uint32_t nlines = tot >> 16;
+        if (sub < (uint32_t)W) {
+            uint32_t acc = S + carry + gpre;
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t v = sub * WPT + i;
+                if (v < (uint32_t)W) s_cnt[v * RS + d_own] = acc;
+                acc += wx[i];
+            }
+        }
+        // the carry from registers into the segment head, whole quads (a quad past the carry's end
+        // lies inside the segment and is overwritten by step 3)
+#pragma unroll
+        for (uint32_t i = 0; i < CPT; i += 4) {
+            if (sub * CPT + i < carry) {
+                *reinterpret_cast<u32x4 *>(&s_k[S + sub * CPT + i]) = u32x4{ck[i], ck[i + 1], ck[i + 2], ck[i + 3]};
+                *reinterpret_cast<u32x4 *>(&s_v[S + sub * CPT + i]) = u32x4{cv[i], cv[i + 1], cv[i + 2], cv[i + 3]};
+            }
+        }
+        if (leader) {
+            s_rec[d_own] = make_uint4(A - LS * G, S - LS * G, (LS << 8) | inv, 0u);
+            if (wl > 0) {
+                s_mark[LS] = (uint8_t)d_own;
+                atomicOr(&s_bits[LS >> 5], 1u << (LS & 31u));
+            }
+        }
+        RS_STAMP(6);
+        __syncthreads();
+        RS_STAMP(1);
+
+        // ---- 3. each whole line's record (its digit from the bitmap: one lookup per line here
+        //      instead of a dependent chain per quad in step 4); stage every slot at base + rank
+        //      (batches of 8: all reads before the stores)
+        for (uint32_t V = t; V < nlines; V += THREADS) {
+            const uint4 rec = s_rec[line_digit(V)];
+            const uint32_t lo = (rec.z >> 8) == V ? (rec.z & 0xFFu) : 0u;
+            s_lrec[V] = make_uint2(rec.x + V * G, (rec.y + V * G) | (lo << 16));
+        }
+        RS_STAMP(2);
+        constexpr int SB = KPT < 8 ? KPT : 8;
+        static_assert(KPT % SB == 0, "whole batches of slots");
+#pragma unroll
+        for (int j0 = 0; j0 < KPT; j0 += SB) {
+            uint32_t pp[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                asm volatile("" : "+v"(key[j]));
+                pp[u] = s_cnt[w * RS + dig(key[j])] + ((j & 1) ? (rk[j / 2] >> 16) : (rk[j / 2] & 0xFFFFu));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int j = j0 + u;
+                uint32_t idx = pp[u];
+                if (!(full || ((uint32_t)(j * kWave) < plim && (j != 0 || h0)))) idx = CAP + 32;  // sink
+                s_k[idx] = key[j];
+                s_v[idx] = val[j];
+            }
+        }
+        __syncthreads();
+        RS_STAMP(3);
+
+        output(S, wl, pending, nlines, cnt);
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            key[j] = nkey[j];
+            val[j] = nval[j];
+        }
     }
     // ---- chunk end: the carries (slots inv .. carry - 1 from the line at g_run - carry)
     if (cbeg < cend) {
@@ -2656,11 +2502,12 @@ __global__ __launch_bounds__(THREADS, ((OPT & 64) && THREADS <= 512) ? 4 : 1) vo
         for (uint32_t i = 0; i < CPT; ++i) {
             const uint32_t x = sub * CPT + i;
             if (x >= inv && x < carry) {
-                a.kout[A + x] = ck[i];
-                a.vout[A + x] = cv[i];
+                hooks::store_word(a.kout + A + x, ck[i]);
+                hooks::store_word(a.vout + A + x, cv[i]);
             }
         }
     }
+    report_order(a.check, order_bad);
     RS_STAMP_FLUSH();
 }
 
@@ -2862,7 +2709,6 @@ static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-#ifndef RSORT_LAB_LITE  // dev labs that instantiate their own variants skip the library's set
 // The compiled scatter kernels. "match" (the default public rank algorithm) runs kRankAtomic, the
 // lane-ordered returning LDS add per key (kRankCount, the ballot peer match, where the lane-order
 // probe fails or RSORT_RANK_BALLOT asks for it); "split" is the reference's 1-bit split sort.
@@ -2984,7 +2830,6 @@ static void *scatter_kernel(int bits, int pairs, int rank, int dmode, int geom, 
     }
 }
 
-#endif  // RSORT_LAB_LITE
 
 // ------------------------------------------------------------------------------ lane-order probe
 // The default ranking (kRankAtomic) rests on gfx950's LDS serving the lanes of one ds_add_rtn_u32
@@ -3117,7 +2962,6 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
     }
 }
 
-#ifndef RSORT_LAB_LITE
 bool scatter_available(int bits, int pairs, int rank_algo, int dmode, int geom) {
     if (geom < 0 || geom >= kGeomCount) return false;
     return scatter_kernel(bits, pairs, rank_algo, dmode, geom, 1) != nullptr;
@@ -3183,7 +3027,6 @@ int scatter_blocks_per_cu(int bits, int pairs, int rank_algo, int geom, int dmod
     return nb;
 }
 
-#endif  // RSORT_LAB_LITE
 
 hipError_t launch_histogram_joint(const HistArgs &a, hipStream_t s) {
     // one 1024-thread workgroup per chunk (the joint table fills the LDS: one per CU)
@@ -3273,13 +3116,3 @@ hipError_t launch_gen_iota(uint32_t *out, uint64_t n, uint32_t base, hipStream_t
 }
 
 }  // namespace rsort
-
-#ifdef RSORT_WG_TIMES
-extern "C" __attribute__((visibility("default"))) int rsort_lab_wg_times(unsigned long long *host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(rsort::g_wg_times), sizeof(rsort::g_wg_times)) == hipSuccess &&
-                   hipMemcpyFromSymbol(host + 8 * 2048 * 4, HIP_SYMBOL(rsort::g_wg_htimes), sizeof(rsort::g_wg_htimes)) ==
-                       hipSuccess
-               ? 0
-               : 6;
-}
-#endif

@@ -7,7 +7,7 @@
 //   1. all-gather every rank's key count; the sampling plan (rsort_multi_sample_plan)
 //   2. a regular sample of the local keys, all-gathered, sorted on the device: the world - 1
 //      global quantile keys (exact key values, not bin edges)
-//   3. splitters with an equal-keys bucket per quantile key (rsort_multi_splitters_make), a
+//   3. splitters with an equal-keys bucket per hot quantile key (rsort_multi_splitters_make_hot), a
 //      stable partition of the local keys into those buckets
 //   4. all-gather of the bucket counts and capacities; the exchange plan (rsort_multi_exchange_plan)
 //      -- identical on every rank, so a capacity error is returned by all ranks together before
@@ -556,18 +556,35 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
             if (sts[r]) return (int)sts[r];
     }
     uint32_t q[kMaxRanks] = {0};
+    int hot[kMaxRanks] = {0};
     if (V > 1 && sp.total > 0) {
         // the rows (each followed by its status word) sorted as one array: the status words are 0
-        // and sort first, so the quantile positions move up by world
+        // and sort first, so the quantile positions move up by world (and the rows' padding, 0xFFFFFFFF,
+        // sorts after the sp.total samples)
         const int64_t ns = (int64_t)world * (int64_t)row;
         profile_pause(1);  // (its passes are part of the plan phase, not the measured local sort)
         local = rsort_u32_device(m.samp_all, m.samp_all, ns, 8, m.sub, m.sub_bytes, s);
         profile_pause(-1);
-        for (int i = 1; i < V && !local; ++i)
-            if (hipMemcpyAsync(&q[i - 1], m.samp_all + world + rsort_multi_quantile_index(&sp, i), 4,
-                               hipMemcpyDeviceToHost, s) != hipSuccess)
-                local = RSORT_ERR_HIP;
+        // each quantile key and the samples hot_reach away on both sides: the key is hot (its own
+        // equal-keys bucket, rsort_multi_splitters_make_hot) when either is the same key
+        const int64_t L = std::max<int64_t>(1, sp.total / ((int64_t)V * 128));
+        uint32_t nb[kMaxRanks][2];
+        for (int i = 1; i < V && !local; ++i) {
+            const int64_t qi = rsort_multi_quantile_index(&sp, i);
+            const int64_t at[3] = {qi, qi - L, qi + L};
+            uint32_t *dst[3] = {&q[i - 1], &nb[i - 1][0], &nb[i - 1][1]};
+            nb[i - 1][0] = nb[i - 1][1] = 0;
+            for (int j = 0; j < 3 && !local; ++j) {
+                if (at[j] < 0 || at[j] >= sp.total) continue;  // (a neighbour outside the samples: not hot there)
+                if (hipMemcpyAsync(dst[j], m.samp_all + world + at[j], 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+                    local = RSORT_ERR_HIP;
+            }
+        }
         if (!local && hipStreamSynchronize(s) != hipSuccess) local = RSORT_ERR_HIP;
+        for (int i = 1; i < V && !local; ++i) {
+            const int64_t qi = rsort_multi_quantile_index(&sp, i);
+            hot[i - 1] = (qi - L >= 0 && nb[i - 1][0] == q[i - 1]) || (qi + L < sp.total && nb[i - 1][1] == q[i - 1]);
+        }
         if (!local) local = injected(me, 1);
         if (local) q[0] = 0xFFFFFFFFu;  // (a failed copy may leave partial quantiles: replaced below)
     }
@@ -575,9 +592,12 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     // still joins the next all-gather with a row of the same size as its peers' and its status in
     // it: it plans on placeholder quantiles (all 0, monotone) instead of its partial ones, and a
     // failure of the pure splitter planning is carried the same way instead of returned.
-    if (local) memset(q, 0, sizeof(q));
+    if (local) {
+        memset(q, 0, sizeof(q));
+        memset(hot, 0, sizeof(hot));
+    }
     rsort_multi_splitters spl;
-    if ((st = rsort_multi_splitters_make(V, q, &spl))) {  // pure, identical on every healthy rank
+    if ((st = rsort_multi_splitters_make_hot(V, q, hot, &spl))) {  // pure, identical on every healthy rank
         if (!local) local = st;
         memset(&spl, 0, sizeof(spl));
         spl.world = V;

@@ -7,7 +7,7 @@ rsort_multi_splitters_make, rsort_multi_exchange_plan), so both paths split and 
 
   1. all_gather of the key counts                      -> the sampling plan (one stride for all)
   2. a regular sample of the local keys (HIP), all_gather, sort (HIP) -> world-1 quantile KEYS
-  3. splitters with an equal-keys bucket per quantile key (world <= 8): a run of equal keys --
+  3. splitters with an equal-keys bucket per hot quantile key (world <= 8): a run of equal keys --
      a hot key, duplicate-heavy input -- is split across ranks in (source rank, position) order
   4. stable partition into those buckets (HIP: rsort_partition_device)
   5. all_gather of the bucket counts and capacities    -> the exchange plan, the same on every
@@ -141,12 +141,15 @@ def dist_sort(keys, k_bits=8, vals=None, ops=None, group=None, capacity=None):
     # 2. sample, gather, sort: the quantile keys
     row = ops.sample(keys, sp.stride, sp.count[rank], sp.row_len)
     q = [0] * (world - 1)
+    hot = None
     gathered = all_gather(row).reshape(-1)
     if world > 1 and sp.total > 0:
         srt = ops.sort_keys(gathered.to(dev))
-        srt = srt.cpu().numpy().view(np.uint32)
-        q = [int(srt[rs.multi_quantile_index(sp, i)]) for i in range(1, world)]
-    spl = rs.multi_splitters(world, q)
+        srt = srt.cpu().numpy().view(np.uint32)[:sp.total]  # (the rows' padding sorts after the samples)
+        qpos = [rs.multi_quantile_index(sp, i) for i in range(1, world)]
+        q = [int(srt[i]) for i in qpos]
+        hot = rs.hot_flags(srt, qpos, world)
+    spl = rs.multi_splitters(world, q, hot)
 
     # 3-4. stable partition into the splitters' buckets
     pk, pv, starts = ops.partition(keys, vals, spl.splitters)

@@ -183,6 +183,7 @@ SIGNATURES = {
     "rsort_plan_check": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_plan_features": ([_PP], _int),
     "rsort_inject_table_fault": ([_int], _int),
+    "rsort_inject_rank_fault": ([_int], _int),
     "rsort_scatter_kernels_used": ([ctypes.c_char_p, _sz, _int], _sz),
     "rsort_profile_begin": ([], _int),
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
@@ -197,6 +198,8 @@ SIGNATURES = {
     "rsort_sample_device": ([_vp, _i64, _i64, _i64, _i64, _vp, _vp], _int),
     "rsort_multi_quantile_index": ([ctypes.POINTER(SamplePlan), _int], _i64),
     "rsort_multi_splitters_make": ([_int, _u32p, ctypes.POINTER(MultiSplitters)], _int),
+    "rsort_multi_splitters_make_hot": ([_int, _u32p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(MultiSplitters)],
+                                       _int),
     "rsort_multi_exchange_plan": ([_int, _int, _int, ctypes.POINTER(_i64), ctypes.POINTER(MultiSplitters),
                                    ctypes.POINTER(_i64), ctypes.POINTER(ExchangePlan)], _int),
     "rsort_u32_multi_transport": ([_vp, _vp, _i64, _vp, _vp, _i64, ctypes.POINTER(_i64), ctypes.POINTER(_i64), _int,
@@ -236,7 +239,12 @@ def _lib() -> ctypes.CDLL:
             raise RuntimeError(f"{LIB_PATH} is not built: run `python cuda.radixsort_amd/build.py` "
                                "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(str(LIB_PATH))
+        # (RSORT_LAB=1 RSORT_LAB_OLD_LIB=1: an older library for a same-box A/B, dev/lab.sh ab -- symbols
+        # added since are left unbound; anywhere else a missing symbol is an error)
+        old = os.environ.get("RSORT_LAB") == "1" and os.environ.get("RSORT_LAB_OLD_LIB") == "1"
         for name, (args, res) in SIGNATURES.items():
+            if old and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
@@ -400,9 +408,23 @@ def table_fault():
         _lib().rsort_inject_table_fault(old)
 
 
+@contextmanager
+def rank_fault():
+    """TEST HOOK (rsort_inject_rank_fault): the lane-ordered scatter kernels swap two ranks per digit in
+    the slot their per-tile rank check reads (a broken lane order); the check must report it."""
+    old = _lib().rsort_inject_rank_fault(1)
+    try:
+        yield
+    finally:
+        _lib().rsort_inject_rank_fault(old)
+
+
+CHECK_TABLE, CHECK_RANK_ORDER = 1, 2
+
+
 def plan_check(p: Plan, ws, stream=None) -> int:
     """The on-device self-checks of the last sort with plan `p` and workspace `ws`
-    (rsort_plan_check; synchronises the stream): 0 = all passed."""
+    (rsort_plan_check; synchronises the stream): 0 = all passed, else CHECK_TABLE / CHECK_RANK_ORDER bits."""
     f = ctypes.c_int()
     _check(_lib().rsort_plan_check(ctypes.byref(p), _ptr(ws), ctypes.byref(f), _stream(stream)), "rsort_plan_check")
     return int(f.value)
@@ -678,10 +700,35 @@ def multi_quantile_index(sp: SamplePlan, i: int) -> int:
     return int(_lib().rsort_multi_quantile_index(ctypes.byref(sp), int(i)))
 
 
-def multi_splitters(world: int, quantile_keys) -> MultiSplitters:
+def multi_splitters(world: int, quantile_keys, hot=None) -> MultiSplitters:
+    """rsort_multi_splitters_make (hot None: every quantile key gets its equal-keys bucket) or
+    rsort_multi_splitters_make_hot (hot: one flag per quantile key)."""
     q = (ctypes.c_uint32 * max(1, world - 1))(*[int(x) & 0xFFFFFFFF for x in quantile_keys])
     out = MultiSplitters()
-    _check(_lib().rsort_multi_splitters_make(int(world), q, ctypes.byref(out)), "rsort_multi_splitters_make")
+    if hot is None:
+        _check(_lib().rsort_multi_splitters_make(int(world), q, ctypes.byref(out)), "rsort_multi_splitters_make")
+    else:
+        h = (ctypes.c_int * max(1, world - 1))(*[1 if x else 0 for x in hot])
+        _check(_lib().rsort_multi_splitters_make_hot(int(world), q, h, ctypes.byref(out)),
+               "rsort_multi_splitters_make_hot")
+    return out
+
+
+def hot_reach(world: int, total_samples: int) -> int:
+    """How far (in samples) a quantile key's run must reach on one side of its quantile position to count
+    as hot (rsort_u32_multi* and multi.py alike): ~1/128 of a rank's share of the sample."""
+    return max(1, int(total_samples) // (int(world) * 128))
+
+
+def hot_flags(sorted_sample, quantile_positions, world: int) -> list[int]:
+    """The hot flag of each quantile key from the sorted sample (numpy): its value also sits hot_reach
+    samples below or above its position."""
+    s = sorted_sample
+    L = hot_reach(world, s.size)
+    out = []
+    for qi in quantile_positions:
+        v = s[qi]
+        out.append(int((qi - L >= 0 and s[qi - L] == v) or (qi + L < s.size and s[qi + L] == v)))
     return out
 
 

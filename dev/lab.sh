@@ -98,7 +98,7 @@ pairs)
     ok_or_stop $? pytest
     grep -E "passed|failed|FAILED|Error" gpurun_out/pairs_tests.log | tail -n 12
     run_bench pairs_new --steps 5 --warmup 2 --keys 16777216 --no-cpu --no-vendor --no-e2e --configs c4,zipf "$@"
-    RSORT_PAIRS64=1 run_bench pairs_64 --steps 5 --warmup 2 --keys 16777216 --no-cpu --no-vendor --no-e2e \
+    RSORT_LAB=1 RSORT_PAIRS64=1 run_bench pairs_64 --steps 5 --warmup 2 --keys 16777216 --no-cpu --no-vendor --no-e2e \
         --configs c4 "$@"
     ;;
 pairslab)
@@ -163,7 +163,9 @@ ab)
     cp cuda.radixsort_amd/librsort.so gpurun_out/ab_new.so
     for side in new "$v" new "$v"; do
         if [ "$side" = new ]; then cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so; else cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so; fi
-        run_bench "ab_$side" --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
+        # (the variant may predate symbols radixsort.py binds: RSORT_LAB_OLD_LIB leaves those unbound)
+        if [ "$side" = new ]; then oldlib=0; else oldlib=1; fi
+        RSORT_LAB=1 RSORT_LAB_OLD_LIB=$oldlib run_bench "ab_$side" --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e \
             --configs "${2:-zipf,c4}" > /dev/null
         python3 - "$side" <<'PY'
 import json, sys
@@ -279,7 +281,7 @@ c2tpc)
     for rep in 1 2; do
         for tpc in ${C2_TPCS:-16 8 4}; do
             for tail in 0 1; do
-                RSORT_NX_TAIL=$tail timeout -k 10 120 python bench.py --keys 67108864 --k 4 --tiles-per-chunk $tpc \
+                RSORT_LAB=1 RSORT_NX_TAIL=$tail timeout -k 10 120 python bench.py --keys 67108864 --k 4 --tiles-per-chunk $tpc \
                     --steps 20 --warmup 5 --no-cpu --no-vendor --no-e2e --configs "" > gpurun_out/c2tpc.json 2> gpurun_out/c2tpc.err
                 stop_unless_ok $? "c2 tpc=$tpc tail=$tail" > /dev/null
                 python3 - "$tpc" "$tail" <<'PY'

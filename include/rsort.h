@@ -188,15 +188,21 @@ RSORT_API int rsort_get_group_chunks(void);
 RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
                                 void *stream);
 /* After a sort with `plan` and `d_workspace` has completed on `stream`: *flags = 0 when every
- * on-device self-check of that sort passed; bit 0 = a k = 3, 4 pass found the next-digit table it
- * reads not holding n keys (the pass then wrote nothing; with RSORT_FEAT_TAIL_SCAN: a tail scan found it
- * so even after an acquire fence and a second sweep) -- the sort's output is then not trustworthy.
- * Synchronises the stream. The sort entry points are stream-ordered and do not
+ * on-device self-check of that sort passed; bit 0 (RSORT_CHECK_TABLE) = a k = 3, 4 pass found the
+ * next-digit table it reads not holding n keys (the pass then wrote nothing; with RSORT_FEAT_TAIL_SCAN:
+ * a tail scan found it so even after an acquire fence and a second sweep); bit 1 (RSORT_CHECK_RANK_ORDER)
+ * = a lane-ordered scatter kernel's per-tile rank check failed: the device no longer served the lanes of
+ * a returning LDS add in lane order (the premise of the default ranking, rsort_lane_order_probe), so
+ * equal digits may have been written out of order -- in either case the sort's output is not
+ * trustworthy. Every plan has the check words (256 B of the workspace); the rank check runs on the first
+ * slot of every full tile of every pass. Synchronises the stream. The sort entry points are stream-ordered and do not
  * wait for the device, so they CANNOT return this check: they return RSORT_OK for such a sort, and
  * this call is the only way to learn of it. rsort_u32_device / rsort_u32_pairs_device use the plan
  * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace. The host
  * entries (rsort_u32, rsort_u32_ex, rsort_u32_pairs) wait for the device anyway: they read the check
  * themselves and return RSORT_ERR_CHECK for such a sort. Never observed failing. */
+#define RSORT_CHECK_TABLE 1
+#define RSORT_CHECK_RANK_ORDER 2
 RSORT_API int rsort_plan_check(const rsort_plan *plan, const void *d_workspace, int *flags, void *stream);
 /* Which carried-histogram scheme a sort with `plan` takes under the current process settings
  * (rsort_set_rank_algo, rsort_set_group_chunks), for outputs the whole-line kernels can write (any
@@ -218,6 +224,12 @@ RSORT_API int rsort_plan_features(const rsort_plan *plan);
  * find the table not holding n keys, write nothing, and record it: rsort_plan_check reports bit 0 and
  * the host entries return RSORT_ERR_CHECK. Process-wide; returns the previous setting. */
 RSORT_API int rsort_inject_table_fault(int enable);
+/* TEST HOOK (never set in production): enable != 0 makes every lane-ordered scatter kernel swap the ranks
+ * of the first two lanes of each digit in the slot its rank check looks at -- what a device serving
+ * same-address LDS adds out of lane order would do. The sort is then unstable (wrong for keys, pairs out
+ * of order), and the check catches it: rsort_plan_check reports bit 1 (RSORT_CHECK_RANK_ORDER), the host
+ * entries return RSORT_ERR_CHECK. Process-wide; returns the previous setting. */
+RSORT_API int rsort_inject_rank_fault(int enable);
 /* The scatter kernel instantiations this library has launched since the last reset, ';'-joined
  * into buf (at most len - 1 characters and a NUL); returns the full length. reset != 0 clears the
  * record. A k = 8 digit-group sort launches a plain and a clustered-input kernel for each pass
@@ -298,6 +310,15 @@ typedef struct rsort_multi_splitters {
     int32_t cut_inside[RSORT_MAX_RANKS];            /* 1: anywhere inside it (equal keys); 0: at its start */
 } rsort_multi_splitters;
 RSORT_API int rsort_multi_splitters_make(int world, const uint32_t *quantile_keys, rsort_multi_splitters *out);
+/* The same with a hot flag per quantile key (hot[r - 1] for boundary r; nullptr: every key hot, which is
+ * rsort_multi_splitters_make). Only a hot key -- one whose run in the sorted sample is long enough that
+ * sending all its copies to one rank would unbalance the ranks -- gets its equal-keys bucket; the others
+ * are plain splitters (boundary r at the start of v_r's bucket: all copies of v_r go to rank r), one
+ * bucket fewer each. Equal consecutive quantile keys are always one hot run. rsort_u32_multi* flags a key
+ * hot when the sample holds it `world * 128`-th of the samples away on either side (a run of >= ~1/64 of
+ * a rank's share): distinct keys get world - 1 splitters instead of 2 (world - 1). */
+RSORT_API int rsort_multi_splitters_make_hot(int world, const uint32_t *quantile_keys, const int *hot,
+                                             rsort_multi_splitters *out);
 
 /* 3. Exchange. counts[s * buckets + b] = keys of rank s's partition in bucket b (the row every
  * rank gathers after partitioning); capacity[r] = output room of rank r. For rank `me`: what it

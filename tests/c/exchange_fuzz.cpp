@@ -59,7 +59,12 @@ int main(int argc, char **argv) {
         }
         std::sort(q.begin(), q.end());
         rsort_multi_splitters sp;
-        if (rsort_multi_splitters_make(world, q.data(), &sp) != RSORT_OK) FAIL("splitters_make failed");
+        // every key hot (rsort_multi_splitters_make) or random hot flags (make_hot)
+        std::vector<int> hot(q.size());
+        for (auto &h : hot) h = (int)(next() & 1);
+        if ((next() & 1) ? rsort_multi_splitters_make(world, q.data(), &sp) != RSORT_OK
+                         : rsort_multi_splitters_make_hot(world, q.data(), hot.data(), &sp) != RSORT_OK)
+            FAIL("splitters_make failed");
         for (int i = 1; i < sp.nsplit; ++i)
             if (sp.split[i] < sp.split[i - 1]) FAIL("splitters not monotone");
         const int buckets = sp.nsplit + 1;

@@ -68,9 +68,12 @@ def _restated_plan(world, counts, splitters, cut_bucket, cut_inside):
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 7, 8, 9, 12, 16])
 def test_plan_matches_restatement(world):
     rng = np.random.default_rng(world)
-    for case in range(40):
+    for case in range(60):
         q = np.sort(rng.integers(0, 64 if case % 2 else 1 << 32, size=max(0, world - 1), dtype=np.uint64))
-        spl = rs.multi_splitters(world, q.tolist())
+        # every key hot (rsort_multi_splitters_make), random hot flags, none hot (make_hot)
+        hot = None if case % 3 == 0 else (rng.random(max(0, world - 1)) < 0.5).tolist() if case % 3 == 1 \
+            else [0] * max(0, world - 1)
+        spl = rs.multi_splitters(world, q.tolist(), hot)
         nb = spl.nsplit + 1
         counts = rng.integers(0, 500, size=(world, nb)) * (rng.random((world, nb)) < 0.7)
         if case % 5 == 0:
@@ -97,6 +100,36 @@ def test_splitters_equal_key_buckets():
     assert rs.multi_splitters(1, []).nsplit == 0
     with pytest.raises(rs.RSortError):
         rs.multi_splitters(3, [5, 4])  # not sorted
+
+
+def test_splitters_hot_flags():
+    """Only hot quantile keys get an equal-keys bucket; the others are plain splitters (boundary at the
+    start of their bucket); a run of equal quantile keys is hot whatever its flags."""
+    spl = rs.multi_splitters(4, [10, 20, 30], hot=[0, 0, 0])
+    assert spl.splitters == [10, 20, 30]
+    assert list(spl.cut_bucket)[1:4] == [1, 2, 3] and list(spl.cut_inside)[1:4] == [0, 0, 0]
+    spl = rs.multi_splitters(4, [10, 20, 30], hot=[0, 1, 0])
+    assert spl.splitters == [10, 20, 21, 30]
+    assert list(spl.cut_bucket)[1:4] == [1, 2, 4] and list(spl.cut_inside)[1:4] == [0, 1, 0]
+    spl = rs.multi_splitters(5, [7, 7, 9, 0xFFFFFFFF], hot=[0, 0, 0, 1])
+    assert spl.splitters == [7, 8, 9, 0xFFFFFFFF]
+    assert list(spl.cut_bucket)[1:5] == [1, 1, 3, 4] and list(spl.cut_inside)[1:5] == [1, 1, 0, 1]
+    # all hot == the flag-less call
+    a = rs.multi_splitters(6, [1, 5, 5, 9, 12], hot=[1] * 5)
+    b = rs.multi_splitters(6, [1, 5, 5, 9, 12])
+    assert a.splitters == b.splitters and list(a.cut_bucket) == list(b.cut_bucket)
+    assert list(a.cut_inside) == list(b.cut_inside)
+
+
+def test_hot_flags_from_sample():
+    """rs.hot_flags (multi.py; rsort_u32_multi* computes the same on the device's sorted sample): a quantile
+    key is hot when the sample holds it hot_reach positions away on either side."""
+    world = 4
+    s = np.sort(np.concatenate([np.arange(0, 3000, 3, dtype=np.uint32), np.full(200, 1500, np.uint32)]))
+    L = rs.hot_reach(world, s.size)
+    assert L == max(1, s.size // (world * 128))
+    pos = [int(np.searchsorted(s, 1500)) + 50, 10, s.size - 5]
+    assert rs.hot_flags(s, pos, world) == [1, 0, 0]
 
 
 def test_capacity_verdict_is_shared():
