@@ -78,8 +78,10 @@ def parse():
                     help="multi-GPU step (c): the whole protocol also at one rank (RSORT_MULTI_FULL: sample, "
                          "partition, self exchange); by default one rank sorts directly")
     ap.add_argument("--dist-overlap", action="store_true",
-                    help="multi-GPU step (c): RSORT_MULTI_OVERLAP (sort each rank's lower half while the upper "
-                         "half is exchanged)")
+                    help="multi-GPU step (c): RSORT_MULTI_OVERLAP at any world (sort each rank's lower half while "
+                         "the upper half is exchanged); by default the library runs it for 2 <= N <= 4 only")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="multi-GPU step (c): RSORT_MULTI_NO_OVERLAP (one half per rank at every world)")
     ap.add_argument("--primitives", action="store_true",
                     help="time the pass primitives in isolation instead (SURVEY 8f row 3) and exit")
     ap.add_argument("--no-group-chunks", action="store_true",
@@ -480,6 +482,50 @@ def is_partition_kernel(name):
     return name.split("<")[0] in ("rs_scatter", "rs_scatter_lines") and len(args) > 5 and args[5] == "1"
 
 
+MULTI_MODEL = "r06_multi_model.json"  # profiles/: the one-GPU component measurements (dev/multi_model.py)
+
+
+def predict_multi_step(model, world, halves, link_gbs):
+    """The multi-GPU step's time per rank predicted from components measured on ONE GPU (DESIGN §5
+    "Predicted N-GPU step"): plan (+ an assumed latency per RCCL all-gather) + partition into the buckets
+    of `world` ranks (2 x world with the overlap's halves) + the exchange, n / world keys per peer over each
+    pair's own xGMI link at `link_gbs`, all links in parallel + the local sort of the 2^30-key arrival.
+    With two halves, each half's exchange moves half the bytes; the lower half's sort runs during the upper
+    half's exchange at the measured CU-shared rate (its time alone / its time beside a stand-in for the
+    exchange's resident kernels), the rest after it; then the upper half's sort. world 1: the direct sort."""
+    if world <= 1:
+        return model["single_gpu_sort_ms"]
+    w = model["worlds"].get(str(world))
+    if w is None:
+        return None
+    base = model["world1_full_protocol_ms"]["ms_plan"] + 3 * model["allgather_latency_ms_assumed"]
+    ex = w["bytes_per_link"] / (link_gbs * 1e9) * 1e3
+    if halves == 1:
+        return base + w["partition_ms"] + ex + w["local_sort_ms"]
+    ov = model["overlap"]["plans"]["default"]
+    half_alone = ov["alone_ms"]
+    shared = ov["contended"].get(f"link_{int(link_gbs)}GBs_wgs8", {}).get("sort_ms", 2 * half_alone)
+    rate = half_alone / shared
+    e_half = ex / 2
+    done = min(half_alone, rate * e_half)
+    return base + w["overlap_partition_ms"] + 2 * e_half + (half_alone - done) + half_alone
+
+
+def multi_prediction(world, halves):
+    """multi.predicted_ms_per_step of the N > 1 line (at the nominal 153-GB/s link rate) and its
+    alternative at the ~64 GB/s RCCL point-to-point rates reach in practice; None without the model."""
+    try:
+        model = json.loads((ROOT / "profiles" / MULTI_MODEL).read_text())
+    except (OSError, ValueError):
+        return None, None
+    main = predict_multi_step(model, world, halves, 153.0)
+    alt = predict_multi_step(model, world, halves, 64.0)
+    return (round(main, 3) if main is not None else None,
+            {"link_64GBs_ms": round(alt, 3) if alt is not None else None, "link_153GBs_ms": round(main, 3)
+             if main is not None else None, "halves": halves,
+             "source": f"profiles/{MULTI_MODEL} (dev/multi_model.py, one GPU) + bench.predict_multi_step"})
+
+
 def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt, steps):
     """The N-GPU block of the line: per-phase ms (mean over the profiled steps per rank, max over
     ranks), the exchange's bytes per rank and per peer link, and the local sort's and the partition's
@@ -509,8 +555,11 @@ def multi_summary(per_rank, world, rank_of_stats, transport, sc, pt, steps):
                 "achieved": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "launches_per_step": t["launches"] // max(1, steps)}
 
+    pred, pred_detail = multi_prediction(world, int(last[0]["halves"]))
     return {
         "transport": transport,
+        "predicted_ms_per_step": pred,
+        "prediction": pred_detail,
         "rccl_world": rank_of_stats.get("rccl_world"),
         "transport_world": int(last[0]["world"]),
         "halves": int(last[0]["halves"]), "exchange_rounds": int(last[0]["rounds"]),
@@ -596,7 +645,8 @@ def main():
     transport = None
     rccl_world = None
     if use_dist and a.dist_impl == "c":
-        rs.set_multi_options((rs.MULTI_FULL if a.dist_full else 0) | (rs.MULTI_OVERLAP if a.dist_overlap else 0))
+        rs.set_multi_options((rs.MULTI_FULL if a.dist_full else 0) | (rs.MULTI_OVERLAP if a.dist_overlap else 0) |
+                             (rs.MULTI_NO_OVERLAP if a.no_overlap and not a.dist_overlap else 0))
         if rehearsal:
             import multi
             host_tr = multi.host_transport()
@@ -838,7 +888,7 @@ def main():
                                    else "k 1-bit splits (kRankSplit)"),
                        "parallelism": "single GPU" if not use_dist else
                        f"range-partition x{world} ({transport}"
-                       f"{', overlap' if a.dist_overlap and a.dist_impl == 'c' else ''}"
+                       f"{', overlap' if a.dist_impl == 'c' and prof_c and multi_stats and multi_stats[-1]['halves'] == 2 else ''}"
                        f"{', full protocol' if a.dist_full and a.dist_impl == 'c' else ''})"},
             "verified": bool(verified),
             "roofline": roof,

@@ -208,7 +208,16 @@ void side_release(SideStream *x) {
 // the communicator is aborted (ncclCommAbort also stops its kernels) and RSORT_ERR_COMM returned.
 std::atomic<int> g_comm_timeout_ms{300000};  // rsort_set_comm_timeout
 std::mutex g_aborted_mu;
-std::vector<void *> g_aborted;  // communicators a timeout aborted (rsort_rccl_comm_destroy skips them)
+// communicators a timeout aborted and nobody has released yet: rsort_u32_multi refuses them and
+// rsort_rccl_comm_destroy only forgets them (ncclCommAbort freed them). An address leaves the list when
+// destroy is called for it and when rsort_rccl_comm_init hands it out again for a new, live communicator
+// (freed communicators' addresses are reused, so a stale entry would refuse a live one)
+std::vector<void *> g_aborted;
+
+void comm_forget(ncclComm_t c) {
+    std::lock_guard<std::mutex> g(g_aborted_mu);
+    g_aborted.erase(std::remove(g_aborted.begin(), g_aborted.end(), (void *)c), g_aborted.end());
+}
 
 bool comm_aborted(ncclComm_t c) {
     std::lock_guard<std::mutex> g(g_aborted_mu);
@@ -506,7 +515,10 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
     // RSORT_MULTI_OVERLAP: every rank's key range is cut in two (H = 2 virtual ranks per rank, the
     // planning functions run for world * H ranks); the lower half is exchanged first and sorted on a
     // side stream while the upper half is exchanged
-    const int H = ((opts & RSORT_MULTI_OVERLAP) && world >= 2 && 2 * world <= kMaxRanks) ? 2 : 1;
+    // (automatic: 2 <= world <= RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD, rsort.h and DESIGN §5)
+    const bool ov = (opts & RSORT_MULTI_OVERLAP) != 0 ||
+                    (!(opts & RSORT_MULTI_NO_OVERLAP) && world <= RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD);
+    const int H = (ov && world >= 2 && 2 * world <= kMaxRanks) ? 2 : 1;
     const int V = world * H;
     auto first_status = [&](const uint64_t *words, size_t stride, size_t at) {
         for (int r = 0; r < world; ++r)
@@ -798,6 +810,7 @@ int rsort_rccl_comm_init(void **comm, int world, int rank, const void *id128, in
     ncclComm_t c = nullptr;
     ncclResult_t r = ncclCommInitRankConfig(&c, world, id, rank, &cfg);
     if (c == nullptr) return RSORT_ERR_COMM;
+    comm_forget(c);  // (a new communicator at the address of one aborted earlier: this one is live)
     const int ms = timeout_ms > 0 ? timeout_ms : g_comm_timeout_ms.load();
     r = nb_complete(c, r, Clock::now() + std::chrono::milliseconds(ms));
     if (r != ncclSuccess) return comm_abort(c);  // (a peer never joined, or setup failed)
@@ -807,7 +820,10 @@ int rsort_rccl_comm_init(void **comm, int world, int rank, const void *id128, in
 
 int rsort_rccl_comm_destroy(void *comm) {
     if (!comm) return RSORT_ERR_ARG;
-    if (comm_aborted((ncclComm_t)comm)) return RSORT_OK;  // released by the abort
+    if (comm_aborted((ncclComm_t)comm)) {  // released by the abort: only forget it
+        comm_forget((ncclComm_t)comm);
+        return RSORT_OK;
+    }
     return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? RSORT_OK : RSORT_ERR_COMM;
 }
 
@@ -839,7 +855,8 @@ int rsort_multi_last_stats(rsort_multi_stats *out) {
 }
 
 int rsort_set_multi_options(int flags) {
-    return g_multi_opts.exchange(flags & (RSORT_MULTI_OVERLAP | RSORT_MULTI_FULL));
+    if ((flags & RSORT_MULTI_OVERLAP) && (flags & RSORT_MULTI_NO_OVERLAP)) return -RSORT_ERR_ARG;
+    return g_multi_opts.exchange(flags & (RSORT_MULTI_OVERLAP | RSORT_MULTI_FULL | RSORT_MULTI_NO_OVERLAP));
 }
 
 int64_t rsort_set_exchange_piece(int64_t keys) {

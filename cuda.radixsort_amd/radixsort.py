@@ -561,12 +561,14 @@ def multi_sort_device(comm, keys, k_bits=8, vals=None, capacity=None, stream=Non
     return kout[:c], (vout[:c] if pairs else None), off.value
 
 
-MULTI_OVERLAP, MULTI_FULL = 1, 2
+MULTI_OVERLAP, MULTI_FULL, MULTI_NO_OVERLAP = 1, 2, 4
+MULTI_AUTO_OVERLAP_MAX_WORLD = 4  # neither overlap flag: the overlap runs for 2 <= world <= this (rsort.h)
 
 
 def set_multi_options(flags: int) -> int:
     """rsort_set_multi_options: MULTI_OVERLAP (sort the lower half of each rank's range while the
-    upper half is exchanged), MULTI_FULL (the whole protocol also at world 1); returns the old flags."""
+    upper half is exchanged) or MULTI_NO_OVERLAP (never; neither flag: the overlap runs for 2 <= world <=
+    MULTI_AUTO_OVERLAP_MAX_WORLD), MULTI_FULL (the whole protocol also at world 1); returns the old flags."""
     return int(_lib().rsort_set_multi_options(int(flags)))
 
 

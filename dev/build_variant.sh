@@ -8,7 +8,8 @@ set -e
 cd /root/repo
 python3 cuda.radixsort_amd/build.py > /dev/null
 mkdir -p dev/build_var
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Iinclude -Icuda.radixsort_amd/csrc"
+# (the lab side of the kernels' hooks: dev/lab_hooks.hpp reads the -D switches in $2)
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -Iinclude -Icuda.radixsort_amd/csrc -DRSORT_LAB_HOOKS=\"../../dev/lab_hooks.hpp\""
 /opt/rocm/bin/hipcc $F $2 -c ${3:-cuda.radixsort_amd/csrc/rsort_kernels.hip} -o dev/build_var/$1.o
 objs=""
 for o in cuda.radixsort_amd/build/*.o; do

@@ -12,8 +12,9 @@
 // Load / store policy: default or non-temporal (__builtin_nontemporal_*), each side separately.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 dev/ceiling_lab.hip -o dev/ceiling_lab
-//   dev/ceiling_lab [log2 keys per buffer = 30] [reps = 10] [pairs]   (JSON lines on stdout; `pairs`: the
-//   pairs pass's write-stream floor, runs of 32 pairs in two arrays, beside runs64 -- VERDICT r4 weak #3)
+//   dev/ceiling_lab [log2 keys per buffer = 30] [reps = 10] [pairs | c2]   (JSON lines on stdout; `pairs`: the
+//   pairs pass's write-stream floor, runs of 32 pairs in two arrays, beside runs64 -- VERDICT r4 weak #3;
+//   `c2`: the C2 pass's write-stream floor, 2^26 keys in runs of 256 into 16 regions -- VERDICT r5 item 3)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -156,6 +157,30 @@ __global__ __launch_bounds__(TH) void runs_pairs(const u32x4 *__restrict__ ink, 
     }
 }
 
+// the k = 4 keys pass's write stream (C2): tiles of TH*Q*4 keys written as RG runs of
+// T/RG keys, run r continuing region r; one chunk of tpc tiles per workgroup (C2: 4096-key tiles, 16 regions,
+// runs of 256 keys, 1024 chunks = 4 workgroups per CU)
+template <int TH, int Q, int RG, bool NTL, bool NTS>
+__global__ __launch_bounds__(TH) void runs_rg(const u32x4 *__restrict__ in, uint32_t *__restrict__ out, uint64_t n,
+                                              uint32_t tpc) {
+    constexpr uint32_t T = TH * Q * 4, L = T / RG;
+    const uint64_t region = n / RG - 32;
+    const uint64_t cbeg = (uint64_t)blockIdx.x * tpc * T;
+    for (uint32_t tile = 0; tile < tpc; ++tile) {
+        const uint64_t tb = cbeg + (uint64_t)tile * T;
+        if (tb + T > n) break;
+        u32x4 v[Q];
+#pragma unroll
+        for (int j = 0; j < Q; ++j) v[j] = ld<NTL>(in + tb / 4 + threadIdx.x + j * TH);
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const uint32_t i = (threadIdx.x + j * TH) * 4;
+            const uint64_t pos = (i / L) * region + (uint64_t)blockIdx.x * tpc * L + (uint64_t)tile * L + (i % L);
+            st<NTS>(reinterpret_cast<u32x4 *>(out + pos), v[j]);
+        }
+    }
+}
+
 // runs64 variants that separate the two sides of the pairs stream's advantage: SPLITR reads each tile as
 // two halves from the two halves of the input (two read streams per workgroup, like keys + values);
 // SPLITW writes the odd digits' runs into a second array (two write arrays, like the pairs stream)
@@ -288,6 +313,28 @@ int main(int argc, char **argv) {
     unsigned long long *rec;
     const int max_wg = cus * 32;
     CK(hipMalloc(&rec, (size_t)max_wg * 4 * 8));
+    if (argc > 3 && argv[3][0] == 'c') {
+        // `c2`: the C2 pass's write-stream floor (2^26 keys, 4096-key tiles, 16 regions, 1024 chunks) beside a
+        // plain one-chunk-per-workgroup copy of the same buffers, loads non-temporal, stores both policies
+        const uint64_t n = 1ull << 26;
+        constexpr int TH = 256, Q = 4;
+        constexpr uint32_t T = TH * Q * 4;
+        const uint64_t tiles = n / T;
+        const uint32_t chunks = 1024, tpc = (uint32_t)(tiles / chunks);
+        const u32x4 *A = (const u32x4 *)a;
+        double ms = timeit([&] { runs_rg<TH, Q, 16, true, true><<<chunks, TH>>>(A, b, n, tpc); });
+        line("c2_runs256_16regions", "chunk", TH, Q, 4, 1, 1, 8.0 * n, ms);
+        ms = timeit([&] { runs_rg<TH, Q, 16, true, false><<<chunks, TH>>>(A, b, n, tpc); });
+        line("c2_runs256_16regions", "chunk", TH, Q, 4, 1, 0, 8.0 * n, ms);
+        ms = timeit([&] { runs_rg<TH, Q, 16, false, false><<<chunks, TH>>>(A, b, n, tpc); });
+        line("c2_runs256_16regions", "chunk", TH, Q, 4, 0, 0, 8.0 * n, ms);
+        const uint64_t c4 = n / 4 / chunks;
+        ms = timeit([&] { copy_chunk<TH, Q, true, true><<<chunks, TH>>>(A, (u32x4 *)b, c4, nullptr); });
+        line("c2_copy", "chunk", TH, Q, 4, 1, 1, 8.0 * n, ms);
+        ms = timeit([&] { copy_chunk<TH, Q, true, false><<<chunks, TH>>>(A, (u32x4 *)b, c4, nullptr); });
+        line("c2_copy", "chunk", TH, Q, 4, 1, 0, 8.0 * n, ms);
+        return 0;
+    }
     if (argc > 3 && argv[3][0] == 'p') {
         // `pairs`: the pairs pass's write-stream floor (8192-pair tiles, runs of 32 pairs in both arrays,
         // one chunk per CU) beside the keys pass's (runs64), 2^lg pairs: four 4 x 2^lg-B buffers

@@ -5,6 +5,8 @@
 # are built on the CPU side first (the command in each file's header); dev/README.md says which
 # DESIGN.md claim each lab backs.
 #
+#   floors           round 6: production scatter passes with / without their stores (dev/floor_lab[_ns]), the C2
+#                    and pairs write-stream floors (dev/ceiling_lab c2 / pairs), the C2 / C4 bench lines
 #   round            pytest -m gpu (all) + the default bench line (what the driver runs at round end)
 #   tests [-k EXPR]  pytest -m gpu, optionally filtered
 #   nodes NODE...    pytest -m gpu on these files / node ids only (-s; LAB_TAG names gpurun_out/nodes_TAG.log)
@@ -72,6 +74,22 @@ kt() {  # tag, bench args...
     stop_unless_ok $? "kt $tag"
 }
 case "$exp" in
+floors)
+    # one pass of each production scatter kernel with and without its output stores
+    # (dev/floor_lab, dev/floor_lab_ns), the C2 and pairs write-stream floors (dev/ceiling_lab c2 / pairs)
+    # and the bench's C2 / C4 lines, all on this one box (gpurun_out/floors.jsonl)
+    : > gpurun_out/floors.jsonl
+    for b in floor_lab floor_lab_ns floor_lab floor_lab_ns; do
+        timeout -k 10 120 dev/$b 10 >> gpurun_out/floors.jsonl 2> gpurun_out/floors.err
+        stop_unless_ok $? "$b"
+    done
+    timeout -k 10 120 dev/ceiling_lab 26 20 c2 >> gpurun_out/floors.jsonl 2>> gpurun_out/floors.err
+    stop_unless_ok $? "ceiling c2"
+    timeout -k 10 200 dev/ceiling_lab 30 10 pairs >> gpurun_out/floors.jsonl 2>> gpurun_out/floors.err
+    stop_unless_ok $? "ceiling pairs"
+    run_bench floors_bench --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e --configs c2,c4 > /dev/null
+    grep -h '"pass"\|c2_\|runs32_pairs\|runs64"' gpurun_out/floors.jsonl
+    ;;
 round)
     timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail 8 --timeout 300 --timeout-method thread \
         > gpurun_out/round_tests.log 2>&1

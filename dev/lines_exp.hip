@@ -17,7 +17,7 @@
 //  16  PRIO   s_setprio 1 for waves 8..15 (the younger half, MI355X_MICROARCH.md item 4)
 //  32  COPY64 carry copy with 8-B LDS accesses (ds_write_b128 costs 13 cycles, b64 6)
 //  64  SB4    staging in batches of 4 slots
-#define RSORT_LAB_LITE
+#define RSORT_LAB_HOOKS "../../dev/lab_hooks.hpp"
 #include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
 
 #include <stdio.h>

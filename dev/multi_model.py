@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/multi_model.json")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--worlds", default="2,4,8")
-    ap.add_argument("--wgs", default="8,16,32,64")
+    ap.add_argument("--wgs", default="8,32")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -117,15 +117,20 @@ def main():
     print("world-1 full protocol", ph, flush=True)
     torch.cuda.empty_cache()
 
-    res["worlds"] = {}
-    for W in [int(x) for x in a.worlds.split(",")]:
-        q = [(i << 32) // W for i in range(1, W)]
-        spl = rs.multi_splitters(W, q)
-        splitters = spl.splitters
+    def partition_ms(V):
+        # the splitters rsort_u32_multi makes for V (virtual) ranks of distinct keys: no quantile key hot
+        q = [(i << 32) // V for i in range(1, V)]
+        splitters = rs.multi_splitters(V, q, hot=[0] * (V - 1)).splitters
         starts = torch.empty(len(splitters) + 2, dtype=torch.int32, device=dev)
         pws = rs.workspace(int(rs._lib().rsort_partition_workspace_size(N, len(splitters) + 1, 0)), dev)
-        tp, tps = timed(lambda: rs.partition_device(keys, out, splitters, starts, ws=pws), a.reps)
+        t, ts = timed(lambda: rs.partition_device(keys, out, splitters, starts, ws=pws), a.reps)
         del pws
+        return t, ts, len(splitters) + 1
+
+    res["worlds"] = {}
+    for W in [int(x) for x in a.worlds.split(",")]:
+        tp, tps, nbk = partition_ms(W)
+        tpo, tpos, nbko = partition_ms(2 * W)  # the overlap's two halves per rank
         arr = range_keys(N, W, W // 2, dev)
         tl, tls = timed(lambda: rs.sort_device(arr, out, 8, ws=ws, plan_=p), a.reps)
         groups = rs.group_flags(p, ws)
@@ -133,7 +138,8 @@ def main():
         torch.cuda.empty_cache()
         per_link = N // W * 4
         sent = (W - 1) * per_link
-        row = {"buckets": len(splitters) + 1, "partition_ms": round(tp, 4), "partition_runs": tps,
+        row = {"buckets": nbk, "partition_ms": round(tp, 4), "partition_runs": tps,
+               "overlap_buckets": nbko, "overlap_partition_ms": round(tpo, 4), "overlap_partition_runs": tpos,
                "local_sort_ms": round(tl, 4), "local_sort_runs": tls,
                "local_sort_group_modes": [("fixed", "groups", "cut")[f] for f in groups],
                "exchange_bytes_sent": sent, "bytes_per_link": per_link, "own_range_bytes": per_link,
@@ -161,7 +167,7 @@ def main():
     side = torch.cuda.Stream(dev)
     plans = {"default": rs.plan(H, 8)}
     tiles = (H + plans["default"].tile_keys - 1) // plans["default"].tile_keys
-    for c in (240, 224, 192):
+    for c in (224,):
         tpc = (tiles + c - 1) // c
         plans[f"fixed{(tiles + tpc - 1) // tpc}"] = rs.plan(H, 8, False, tpc)
     hws = rs.workspace(max(pp.workspace_bytes for pp in plans.values()), dev)

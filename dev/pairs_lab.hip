@@ -9,9 +9,10 @@
 //         dev/pairs_lab.hip -o dev/pairs_lab && dev/pairs_lab [lg=30]
 //   PL_ZIPF=1: Zipf(s=1) keys over 2^20 ranks (the C4 workload); PL_PASS=1: time pass 1 (digit 1) on
 //   pass 0's output (clustered for Zipf keys); PL_REPS=n.
-#define RSORT_LAB_LITE
 #define RSORT_STAMPS
+#define RSORT_LAB_HOOKS "../../dev/lab_hooks.hpp"
 #include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
+#include "pairs_variants.hpp"
 
 #include <math.h>
 #include <stdio.h>
@@ -169,12 +170,12 @@ int main(int argc, char **argv) {
              rs_scatter_pairs<8, 1024, 8, 1><<<g, 1024>>>(x); }, 1e9f, {}},
         {"rs_scatter_pairs 512 x 8 seq. staging, 512 ch", [](const ScatterArgs &x, uint32_t g) {
              (void)x; (void)g;
-             rs_scatter_pairs<8, 512, 8, 0, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
+             rs_scatter_pairs_lab<8, 512, 8, 0, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
         {"rs_scatter_pairs 512 x 8 seq. staging CL", [](const ScatterArgs &x, uint32_t g) {
              (void)x; (void)g;
-             rs_scatter_pairs<8, 512, 8, 1, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
+             rs_scatter_pairs_lab<8, 512, 8, 1, 1, 64><<<g_sb2.num_chunks, 512>>>(g_sb2); }, 1e9f, {}},
         {"rs_scatter_pairs 1024 x 8 seq. staging, 256 ch", [](const ScatterArgs &x, uint32_t g) {
-             rs_scatter_pairs<8, 1024, 8, 1, 1, 64><<<g, 1024>>>(x); }, 1e9f, {}},
+             rs_scatter_pairs_lab<8, 1024, 8, 1, 1, 64><<<g, 1024>>>(x); }, 1e9f, {}},
     };
     const int rounds = env_int("PL_ROUNDS", 3);
     std::vector<uint32_t> refk(n), refv(n), gk(n), gv(n);

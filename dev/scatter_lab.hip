@@ -5,9 +5,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc \
 //         dev/scatter_lab.hip -o dev/scatter_lab && dev/scatter_lab [log2n]
-#ifdef LINES_ONLY
-#define RSORT_LAB_LITE
-#endif
+#define RSORT_LAB_HOOKS "../../dev/lab_hooks.hpp"
 #include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
 
 #include <stdio.h>

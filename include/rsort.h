@@ -400,12 +400,18 @@ RSORT_API int rsort_set_comm_timeout(int timeout_ms);
  *  RSORT_MULTI_OVERLAP  every rank's key range is cut in two at a sampled quantile (the planning
  *                       functions run for 2 x world ranks, world <= 8): the lower halves are
  *                       exchanged first, and each rank sorts its lower half on a second stream
- *                       while the upper halves are exchanged; same output. Off by default.
+ *                       while the upper halves are exchanged; same output.
+ *  RSORT_MULTI_NO_OVERLAP  never cut the ranges in two.
+ *  Neither: the overlap runs for 2 <= world <= 4 (RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD) and not above, where
+ *                       its 2 x world buckets make the partition cost more than the half sort it hides
+ *                       (measured on one GPU, partition 5.4 vs 3.1 ms at world 8).
  *  RSORT_MULTI_FULL     run the whole protocol also at world 1 (sample, partition into one
  *                       bucket, self exchange): for tests and overhead measurements. By default
  *                       one rank sorts its keys directly (the partition would be a copy). */
 #define RSORT_MULTI_OVERLAP 1
 #define RSORT_MULTI_FULL 2
+#define RSORT_MULTI_NO_OVERLAP 4
+#define RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD 4
 RSORT_API int rsort_set_multi_options(int flags);
 
 /* Per-phase record of a multi-GPU sort (rsort_u32_multi*), for the N-GPU bench line. Off by
@@ -421,7 +427,7 @@ RSORT_API int rsort_set_multi_options(int flags);
 typedef struct rsort_multi_stats {
     int32_t world;       /* ranks of the communicator (rsort_u32_multi: ncclCommCount) */
     int32_t rank;        /* this rank (rsort_u32_multi: ncclCommUserRank) */
-    int32_t halves;      /* 1, or 2 under RSORT_MULTI_OVERLAP */
+    int32_t halves;      /* 1, or 2 when the overlap ran (RSORT_MULTI_OVERLAP, or its automatic use) */
     int32_t direct;      /* 1: world 1 without RSORT_MULTI_FULL, sorted directly (phases: local_sort) */
     int64_t rounds;      /* exchange rounds (messages per peer and array) */
     int64_t bytes_per_key; /* 4 (keys) or 8 (key + value) */

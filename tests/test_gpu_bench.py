@@ -122,6 +122,10 @@ def check_multi_block(d, world):
     assert any(is_partition_kernel(k) for k in d["config"]["scatter_kernels"])
     if world > 1:
         assert m["partition_scatter"] is not None and m["partition_scatter"]["avg_launch_ms"] > 0
+    # the component-measured prediction the first real N-GPU run is checked against
+    # (profiles/r06_multi_model.json; world 1: the direct sort)
+    assert m["predicted_ms_per_step"] is not None and m["predicted_ms_per_step"] > 0
+    assert m["prediction"]["halves"] == m["halves"] and m["prediction"]["link_64GBs_ms"] >= m["predicted_ms_per_step"]
 
 
 def test_bench_plain_gpus2_self_launches_rehearsal():
@@ -145,6 +149,11 @@ def test_bench_gpus2_overlap_pairs_rehearsal():
     assert d["n_gpus"] == 2 and d["verified"] is True
     check_multi_block(d, 2)
     assert d["multi"]["halves"] == 2 and d["multi"]["exchange"]["bytes_per_key"] == 8
+    assert ", overlap" in d["config"]["parallelism"]
+    # --no-overlap: one half per rank (the default at N = 2 is the overlap, rsort.h)
+    d = run_bench_env({"RSORT_BENCH_BACKEND": "gloo"}, "--gpus", "2", "--steps", "1", "--warmup", "1",
+                      "--keys", str(1 << 21), "--no-overlap", "--no-cpu")
+    assert d["verified"] is True and d["multi"]["halves"] == 1 and ", overlap" not in d["config"]["parallelism"]
 
 
 def test_bench_one_rank_rccl_reports_phases():

@@ -220,7 +220,9 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0, stats=Non
         stats.extend([None] * world)
         rs.multi_set_profiling(True)
     old_piece = rs.set_exchange_piece(piece) if piece else None
-    old_opts = rs.set_multi_options(opts)
+    # (opts 0: one half per rank, MULTI_NO_OVERLAP -- the automatic overlap has its own test; None: no
+    # overlap flag at all, the library's automatic choice)
+    old_opts = rs.set_multi_options(0 if opts is None else opts if opts else rs.MULTI_NO_OVERLAP)
     dev_in = [(rs.from_numpy_u32(kx), rs.from_numpy_u32(vx) if vx is not None else None) for kx, vx in inputs]
     res = [None] * world
 
@@ -446,6 +448,24 @@ def test_c_multi_loopback_overlap(world, dist_name, pairs, k, piece):
         assert np.abs(sizes - keys.size / world).max() <= 0.05 * keys.size / world + 64, sizes
 
 
+@pytest.mark.parametrize("world,halves", [(2, 2), (4, 2), (5, 1)])
+def test_c_multi_loopback_automatic_overlap(world, halves):
+    """Round 6: without an overlap flag the lower-half overlap runs for 2 <= world <= 4
+    and not above (its 2 x world buckets cost the partition more than the hidden half sort at
+    world 8). Same output either way."""
+    sys.path.insert(0, str(PKG))
+    import radixsort as rs
+    inputs = [_loopback_inputs(r, 150_000, "zipf", True) for r in range(world)]
+    st = []
+    res = _run_loopback(world, inputs, 8, stats=st, opts=None)
+    assert all(isinstance(x, tuple) for x in res), res
+    assert [x["halves"] for x in st] == [halves] * world
+    keys = np.concatenate([i[0] for i in inputs])
+    rk, rv = oracle_sort_pairs(keys, np.concatenate([i[1] for i in inputs]), 8)
+    assert np.array_equal(np.concatenate([x[0] for x in res]), rk)
+    assert np.array_equal(np.concatenate([x[1] for x in res]), rv)
+
+
 def test_c_multi_loopback_capacity_on_every_rank():
     """one rank's output too small -> EVERY rank returns RSORT_ERR_CAPACITY
     before any key moves (no rank is left waiting in the exchange)."""
@@ -522,20 +542,34 @@ try:
     print("JOINED")
 except rs.RSortError as e:
     print(f"STATUS {e.status} {time.monotonic() - t0:.1f}")
+# ADVICE r5: a retry in the same process -- a new communicator (possibly at the aborted one's address) sorts
+# and is destroyed normally
+c = rs.RcclComm(1, 0, rs.rccl_unique_id(), timeout_ms=20000)
+keys = torch.randint(-2**31, 2**31 - 1, (300000,), dtype=torch.int32, device="cuda")
+with rs.multi_options(rs.MULTI_FULL):
+    ok, _, off = rs.multi_sort_device(c, keys, 8)
+got = ok.cpu().numpy().view("uint32")
+want = keys.cpu().numpy().view("uint32")
+import numpy as np
+print("RETRY", int(np.array_equal(got, np.sort(want))), off)
+c.close()
+print("DESTROYED")
 """
 
 
 def test_rccl_init_deadline_when_a_peer_never_joins():
     """VERDICT r4 #2: the communicator is set up non-blocking (ncclCommInitRankConfig, blocking = 0)
     and polled; rank 0 of a world-2 communicator whose rank 1 never joins gets RSORT_ERR_COMM after
-    its 5-s deadline (the setup is aborted) instead of waiting forever. In a subprocess, so a hang in
-    RCCL's abort could only fail this test."""
+    its 5-s deadline (the setup is aborted) instead of waiting forever; then, in the same process, a new
+    communicator sorts and is destroyed (ADVICE r5: the aborted one's address may come back). In a
+    subprocess, so a hang in RCCL's abort could only fail this test."""
     import subprocess
     r = subprocess.run([sys.executable, "-c", _INIT_SNIPPET, str(PKG)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith(("STATUS", "JOINED"))]
     assert line and line[0].startswith("STATUS 10"), r.stdout[-1000:]
     assert 4.0 <= float(line[0].split()[2]) < 60.0, line
+    assert "RETRY 1 0" in r.stdout and "DESTROYED" in r.stdout, r.stdout[-1000:]
 
 
 def test_rccl_comm_timeout_setting():
