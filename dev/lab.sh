@@ -90,6 +90,21 @@ floors)
     run_bench floors_bench --steps 10 --warmup 3 --no-cpu --no-vendor --no-e2e --configs c2,c4 > /dev/null
     grep -h '"pass"\|c2_\|runs32_pairs\|runs64"' gpurun_out/floors.jsonl
     ;;
+partab)
+    # the multi-GPU partition (dev/part_lab.py: 2^30 keys into the buckets of N ranks) with the box's
+    # librsort.so and dev/var_$1.so, alternating twice
+    v=$1
+    cp cuda.radixsort_amd/librsort.so gpurun_out/ab_new.so
+    for side in new "$v" new "$v"; do
+        if [ "$side" = new ]; then cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so; oldlib=0
+        else cp "dev/var_$v.so" cuda.radixsort_amd/librsort.so; oldlib=1; fi
+        RSORT_LAB=1 RSORT_LAB_OLD_LIB=$oldlib timeout -k 10 200 python dev/part_lab.py > gpurun_out/partab_$side.log 2>&1
+        stop_unless_ok $? "part_lab $side"
+        echo "$side $(tail -n 1 gpurun_out/partab_$side.log)"
+    done
+    cp gpurun_out/ab_new.so cuda.radixsort_amd/librsort.so
+    rm -f gpurun_out/ab_new.so
+    ;;
 round)
     timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail 8 --timeout 300 --timeout-method thread \
         > gpurun_out/round_tests.log 2>&1
