@@ -793,6 +793,25 @@ int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flag
     return RSORT_OK;
 }
 
+int rsort_cut_plan_stats(const rsort_plan *plan, const void *d_workspace, int *stats, void *stream) {
+    if (!plan || !stats || !d_workspace) return RSORT_ERR_ARG;
+    int st = check_plan(plan);
+    if (st) return st;
+    for (int i = 0; i < 8; ++i) stats[i] = 0;
+    if (!joint_plan(*plan) || plan->n == 0) return RSORT_OK;
+    const Carve c = carve(*plan, const_cast<void *>(d_workspace));
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    for (int i = 0; i < 2; ++i)
+        if (2 * i + 1 < plan->passes &&
+            hipMemcpyAsync(h[i], c.bounds + i * kBoundsWords + kBoundsStat, 16, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 4; ++j) stats[4 * i + j] = (int)h[i][j];
+    return RSORT_OK;
+}
+
 int rsort_plan_features(const rsort_plan *plan) {
     if (check_plan(plan) != RSORT_OK) return -RSORT_ERR_ARG;
     const rsort_plan &p = *plan;

@@ -170,7 +170,11 @@ hipError_t launch_histogram(int bits, int dmode, const HistArgs &a, hipStream_t 
 // p + 1 reads no keys for its histogram.
 constexpr int kJointBits = 8;
 constexpr uint32_t kJointBins = 1u << kJointBits;
-constexpr uint32_t kBoundsWords = kJointBins + 2;  // {flag, chunk starts[0..R]}
+// {flag, chunk starts[0..R], the cut plan's stats}: rs_joint_bounds writes, per odd pass, how its cut plan
+// takes its pieces -- key ranges, row tasks (summed joint-count rows), direct adds, negatively counted ranges
+// (all 0 for whole groups / fixed chunks); rsort_cut_plan_stats reads them
+constexpr uint32_t kBoundsStat = kJointBins + 2;
+constexpr uint32_t kBoundsWords = kBoundsStat + 4;
 // bounds[0]: how the next pass takes its chunks
 //   kGroupsFixed  fixed chunks, histogram counted from the keys (group path off)
 //   kGroupsWhole  the digit groups are the chunks (each fits max_keys): table = joint counts

@@ -1045,6 +1045,7 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
     __shared__ uint32_t s_slot[R];                 // counted pieces' slots
     __shared__ uint32_t s_rows;                    // every chunk wrote its joint-count rows
     const uint32_t t = threadIdx.x;
+    if (t < 4) bounds[kBoundsStat + t] = 0u;       // (the cut plan's stats: none unless one is made below)
     if (t == 0) {
         // (read and re-armed for the next joint count; the other threads read s_rows after a barrier)
         s_rows = (rows_cnt != nullptr && ctab != nullptr && rowone != nullptr && *rows_cnt == R) ? 1u : 0u;
@@ -1332,11 +1333,23 @@ __global__ __launch_bounds__(1024) void rs_joint_bounds(const uint32_t *joint, c
         }
     }
     np = min(np, kPlanMaxRanges);  // (cannot exceed it: <= 255 counted pieces, 2 ranges each)
+    // the plan's make-up for rsort_cut_plan_stats (tests): direct adds and negatively counted ranges
+    auto ndirect = [](const Split &x) { return (x.dl[0] > 0u ? 1u : 0u) + (x.dl[1] > 0u ? 1u : 0u); };
+    auto nneg = [](const Split &x) {
+        return (x.neg[0] && x.e[0] > x.b[0] ? 1u : 0u) + (x.neg[1] && x.e[1] > x.b[1] ? 1u : 0u);
+    };
+    uint32_t ndir = 0, nng = 0;
+    (void)block_excl_scan<1024>(t < R ? ndirect(hs) + ndirect(ts) : 0u, s_ws, ndir);
+    (void)block_excl_scan<1024>(t < R ? nneg(hs) + nneg(ts) : 0u, s_ws, nng);
     if (t == 0) {
         plan[0] = np;
         plan[1] = K;
         plan[2] = nr;
         bounds[0] = kGroupsCut;
+        bounds[kBoundsStat] = np;
+        bounds[kBoundsStat + 1] = nr - ndir;
+        bounds[kBoundsStat + 2] = ndir;
+        bounds[kBoundsStat + 3] = nng;
     }
     __syncthreads();
     // the counted pieces' rows and each cut group's derived row start at zero (the histogram

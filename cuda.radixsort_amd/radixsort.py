@@ -181,6 +181,7 @@ SIGNATURES = {
     "rsort_group_flags": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_lane_order_probe": ([], _int),
     "rsort_plan_check": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
+    "rsort_cut_plan_stats": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], _int),
     "rsort_plan_features": ([_PP], _int),
     "rsort_inject_table_fault": ([_int], _int),
     "rsort_inject_rank_fault": ([_int], _int),
@@ -385,6 +386,15 @@ def group_flags(p: Plan, ws, stream=None) -> list[int]:
     flags = (ctypes.c_int * 2)()
     _check(_lib().rsort_group_flags(ctypes.byref(p), _ptr(ws), flags, _stream(stream)), "rsort_group_flags")
     return [int(flags[0]), int(flags[1])]
+
+
+def cut_plan_stats(p: Plan, ws, stream=None) -> list[dict]:
+    """How the last sort's cut plans (passes 1 and 3) took their pieces' counts (rsort_cut_plan_stats;
+    synchronises the stream): per pass {key_ranges, row_tasks, direct_adds, negative_ranges}."""
+    st = (ctypes.c_int * 8)()
+    _check(_lib().rsort_cut_plan_stats(ctypes.byref(p), _ptr(ws), st, _stream(stream)), "rsort_cut_plan_stats")
+    keys = ("key_ranges", "row_tasks", "direct_adds", "negative_ranges")
+    return [{k: int(st[4 * i + j]) for j, k in enumerate(keys)} for i in range(2)]
 
 
 FEAT_GROUPS, FEAT_NEXT_DIGIT, FEAT_RAW_TABLES, FEAT_TAIL_SCAN = 1, 2, 4, 8

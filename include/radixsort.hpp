@@ -48,6 +48,10 @@ inline void sortByThrust(const uint32_t *in, int n, uint32_t *out) {
     RSORT_CHECK(rsort_u32_vendor(in, out, (int64_t)n));
 }
 
+// blockSize is accepted and has NO effect: the reference sets its tile size from it (T = 2 * blockSize,
+// Parallel7.cu:541; Parallel1-6 T = blockSize), here the gfx950 tile geometry is chosen per digit width,
+// key count and pairs. The sorted output is unique, so no result depends on it; only the
+// reference's per-phase times do (tools/rsort_cli still prints the "Block size" line it was given).
 inline void sortByDevice(const uint32_t *h_input, int n, uint32_t *h_output, int numBits,
                          int blockSize) {
     rsort_phase_times t;

@@ -121,6 +121,12 @@ RSORT_API int rsort_version(void); /* major * 10000 + minor * 100 + patch */
  * CU count and the scatter kernel's occupancy (a fixed default when no device is visible). */
 RSORT_API int rsort_plan_make(int64_t n, int k_bits, int pairs, int64_t tiles_per_chunk,
                               rsort_plan *plan);
+/* Workspace bytes of a device sort: the ping-pong keys (4n, and 4n more for values), the chunk table and
+ * scan sums (a few hundred KB), 256 B of check words, and by plan kind: k = 8 plans with 256 chunks (every
+ * 2^23..2^31-key sort on a 256-CU MI355X) a FIXED ~65 MiB more -- the joint counts (256 KB), the cut plan
+ * and its piece counts (~0.5 MB) and the per-chunk joint-count rows (256^3 words = 64 MiB + 256 KB), which
+ * only skewed chunks write but every such plan reserves (near 2^23 keys that is more than the keys); k = 3,
+ * 4 plans two more chunk tables. */
 RSORT_API size_t rsort_workspace_size(int64_t n, int k_bits, int pairs);
 
 /* ---------------------------------------------------------------- whole sort, device */
@@ -140,8 +146,9 @@ RSORT_API int rsort_sort_planned(const rsort_plan *plan, const uint32_t *d_keys_
 /* Synchronous drop-in for sortByDevice (Parallel7.cu:530): H2D, sort, D2H on the current
  * device with a library-owned, per-device cached workspace. */
 RSORT_API int rsort_u32(const uint32_t *in, uint32_t *out, int64_t n, int k_bits);
-/* Same; block_size is accepted for signature compatibility (the gfx950 tile geometry is
- * fixed per k); `times` (may be NULL) receives the per-phase kernel times of this call. */
+/* Same; block_size is accepted for signature compatibility and has NO effect (the reference sets its
+ * tile size from it, Parallel7.cu:541; here the gfx950 tile geometry follows k, n and pairs); `times`
+ * (may be NULL) receives the per-phase kernel times of this call. */
 RSORT_API int rsort_u32_ex(const uint32_t *in, uint32_t *out, int64_t n, int k_bits,
                            int block_size, rsort_phase_times *times);
 RSORT_API int rsort_u32_pairs(const uint32_t *keys_in, const uint32_t *vals_in,
@@ -187,6 +194,13 @@ RSORT_API int rsort_get_group_chunks(void);
  * without them). Synchronises the stream. */
 RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace, int *flags,
                                 void *stream);
+/* After a k = 8 digit-group sort with `plan` and `d_workspace` has completed on `stream`: how the cut plans
+ * of passes 1 and 3 (rsort_group_flags 2) took the counts of their pieces, stats[4 * i + j] for pass 2i+1:
+ * j = 0 key ranges counted from the keys, 1 row tasks (sums of the previous pass's per-chunk joint-count
+ * rows), 2 direct adds (a chunk part whose keys all share one next digit), 3 key ranges counted negatively
+ * (the complement of a piece inside a chunk). All 0 for a pass on whole groups or fixed chunks, and for
+ * plans without digit groups. Synchronises the stream (tests and diagnostics). */
+RSORT_API int rsort_cut_plan_stats(const rsort_plan *plan, const void *d_workspace, int *stats, void *stream);
 /* After a sort with `plan` and `d_workspace` has completed on `stream`: *flags = 0 when every
  * on-device self-check of that sort passed; bit 0 (RSORT_CHECK_TABLE) = a k = 3, 4 pass found the
  * next-digit table it reads not holding n keys (the pass then wrote nothing; with RSORT_FEAT_TAIL_SCAN:
@@ -195,7 +209,7 @@ RSORT_API int rsort_group_flags(const rsort_plan *plan, const void *d_workspace,
  * a returning LDS add in lane order (the premise of the default ranking, rsort_lane_order_probe), so
  * equal digits may have been written out of order -- in either case the sort's output is not
  * trustworthy. Every plan has the check words (256 B of the workspace); the rank check runs on the first
- * slot of every full tile of every pass. Synchronises the stream. The sort entry points are stream-ordered and do not
+ * slot of every 8th full tile of each chunk (its first included), every pass. Synchronises the stream. The sort entry points are stream-ordered and do not
  * wait for the device, so they CANNOT return this check: they return RSORT_OK for such a sort, and
  * this call is the only way to learn of it. rsort_u32_device / rsort_u32_pairs_device use the plan
  * rsort_plan_make(n, k_bits, pairs, 0) gives, so pass that plan and the same workspace. The host

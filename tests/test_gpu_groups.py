@@ -28,6 +28,9 @@ def group_plan(n, pairs=False):
     return p
 
 
+_LAST_STATS = [None]  # run(): the last sort's rsort_cut_plan_stats
+
+
 def run(x, p, vals=None, groups=True):
     with rs.group_chunks(groups):
         d_in = rs.from_numpy_u32(x)
@@ -36,12 +39,14 @@ def run(x, p, vals=None, groups=True):
         if vals is None:
             rs.sort_device(d_in, d_out, 8, ws=ws, plan_=p)
             flags = rs.group_flags(p, ws)
+            _LAST_STATS[0] = rs.cut_plan_stats(p, ws)
             assert np.array_equal(rs.to_numpy_u32(d_in), x), "input buffer was modified"
             return rs.to_numpy_u32(d_out), flags
         v_in = rs.from_numpy_u32(vals)
         v_out = rs.empty_u32(x.size)
         rs.sort_device(d_in, d_out, 8, vals_in=v_in, vals_out=v_out, ws=ws, plan_=p)
         flags = rs.group_flags(p, ws)
+        _LAST_STATS[0] = rs.cut_plan_stats(p, ws)
         return (rs.to_numpy_u32(d_out), rs.to_numpy_u32(v_out)), flags
 
 
@@ -177,6 +182,10 @@ def test_cut_plan_rows_with_spills():
             y, flags = run(x, group_plan(n))
             assert np.array_equal(y, oracle_sort(x, 8))
         assert flags[0] == 2
+        # the pieces really came from the rows (a fallback to counting them from the keys would
+        # pass the checks above too): pass 1's cut plan summed rows
+        st = _LAST_STATS[0]
+        assert st[0]["row_tasks"] > 0, st
 
 
 @pytest.mark.parametrize("pairs", [False, True])
@@ -198,6 +207,13 @@ def test_cut_plan_rows_hot_key_runs(pairs):
         y, flags = run(x, group_plan(n))
         assert np.array_equal(y, oracle_sort(x, 8))
     assert list(flags) == [2, 2]
+    # every piece kind was emitted -- row tasks, direct adds (pass 3: chunks of nothing but the
+    # hot key's copies) and ranges counted negatively -- not a silent fallback to counting from the keys
+    st = _LAST_STATS[0]
+    print("cut plan stats", st)
+    assert st[0]["row_tasks"] > 0 and st[1]["row_tasks"] > 0, st
+    assert st[1]["direct_adds"] > 0, st
+    assert st[0]["negative_ranges"] + st[1]["negative_ranges"] > 0, st
 
 
 def test_empty_groups():
