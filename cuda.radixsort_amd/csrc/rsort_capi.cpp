@@ -945,6 +945,23 @@ int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *d_vals_in,
                                            (uint64_t)n, d_bucket_starts, s));
 }
 
+int rsort_partition_check(int64_t n, int num_buckets, int pairs, const void *d_workspace, int *flags, void *stream) {
+    if (!flags || !d_workspace || num_buckets < 1 || num_buckets > kMaxSplitters + 1) return RSORT_ERR_ARG;
+    *flags = 0;
+    rsort_plan p;
+    int st = plan_fill(n < 0 ? 0 : n, partition_bits(n < 0 ? 0 : n, num_buckets, pairs ? 1 : 0), pairs ? 1 : 0, 0, &p,
+                       /*partition=*/1);
+    if (st) return st;
+    if (n <= 0) return RSORT_OK;
+    const Carve c = carve(p, const_cast<void *>(d_workspace));
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t h = 0;
+    if (hipMemcpyAsync(&h, c.done + kDoneErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return RSORT_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return RSORT_ERR_HIP;
+    *flags = (int)(h & (kCheckTable | kCheckRankOrder));
+    return RSORT_OK;
+}
+
 int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits, uint32_t *d_hist,
                         void *d_workspace, size_t workspace_bytes, void *stream) {
     rsort_plan p;

@@ -625,6 +625,11 @@ int multi_sort(const uint32_t *d_keys, const uint32_t *d_vals, int64_t n, uint32
         local = rsort_partition_device(d_keys, d_vals, m.part_k, m.part_v, n, spl.split, buckets, m.starts, m.sub,
                                        m.sub_bytes, s);
     if (!local) local = d2h(starts, m.starts, (size_t)(buckets + 1) * 4, s);
+    if (!local) {  // the partition's self-check (its scatter's rank check): a failure stops every rank below
+        int pf = 0;
+        local = rsort_partition_check(n, buckets, d_vals != nullptr ? 1 : 0, m.sub, &pf, s);
+        if (!local && pf) local = RSORT_ERR_CHECK;
+    }
 
     // 4. count matrix + capacities + statuses -> the exchange plans (the same on every rank). The
     //    row has a fixed size whatever this rank's bucket count (a failed rank's may differ), so the

@@ -190,6 +190,7 @@ SIGNATURES = {
     "rsort_profile_end": ([ctypes.POINTER(PhaseTimes)], _int),
     "rsort_partition_workspace_size": ([_i64, _int, _int], _sz),
     "rsort_partition_device": ([_vp, _vp, _vp, _vp, _i64, _u32p, _int, _vp, _vp, _sz, _vp], _int),
+    "rsort_partition_check": ([_i64, _int, _int, _vp, ctypes.c_void_p, _vp], _int),
     "rsort_top_histogram": ([_vp, _i64, _int, _vp, _vp, _sz, _vp], _int),
     "rsort_top_histogram_sampled": ([_vp, _i64, _int, _int, _vp, _vp], _int),
     "rsort_multi_workspace_size": ([_i64, _i64, _int, _int, _int], _sz),
@@ -816,6 +817,14 @@ def partition_device(keys_in, keys_out, splitters, bucket_starts, vals_in=None, 
     _check(_lib().rsort_partition_device(_ptr(keys_in), _ptr(vals_in), _ptr(keys_out), _ptr(vals_out), n, sp, nb,
                                          _ptr(bucket_starts), _ptr(ws), ws.numel(), _stream(stream)),
            "rsort_partition_device")
+
+
+def partition_check(n: int, num_buckets: int, pairs: bool, ws, stream=None) -> int:
+    """rsort_partition_check: the last partition's on-device self-check in `ws` (0 = passed)."""
+    f = ctypes.c_int()
+    _check(_lib().rsort_partition_check(int(n), int(num_buckets), 1 if pairs else 0, _ptr(ws), ctypes.byref(f),
+                                        _stream(stream)), "rsort_partition_check")
+    return int(f.value)
 
 
 def top_histogram_sampled(keys, top_bits, stride, hist, stream=None):

@@ -142,6 +142,49 @@ int main(int argc, char **argv) {
         line("c2_keys_middle_pass", n, 8, best_of(reps * 4, 3, [&] {
                  rs_scatter_lines<4, 256, 16, kLineKeys, false, kDigitShift, 1><<<(unsigned)chunks, 256>>>(a);
              }));
+        // the same middle pass as a sort runs it: its offsets from the raw next-digit counts the pass before
+        // added (every workgroup sums the whole 16 x 1024 table, raw_offsets), on that pass's output. Pass 0
+        // (k0 -> k1) counts digit 1 into `next`; pass 1 (k1, shift 4) then reads `next` raw, counts into t2,
+        // clears t3 (the tables stay consistent with k1 on every repeat: only t2 accumulates)
+#ifndef RSORT_LAB_NO_STORES
+        uint32_t *t2, *t3;
+        CK(hipMalloc(&t2, 16 * chunks * 4));
+        CK(hipMalloc(&t3, 16 * chunks * 4));
+        CK(hipMemset(next, 0, 16 * chunks * 4));
+        CK(hipMemset(t2, 0, 16 * chunks * 4));
+        ScatterArgs p0 = a;
+        p0.next_table = next;
+        rs_scatter_lines<4, 256, 16, kLineKeys, false, kDigitShift, 1><<<(unsigned)chunks, 256>>>(p0);
+        CK(hipDeviceSynchronize());
+        ScatterArgs p1 = a;
+        p1.kin = k1;
+        p1.kout = k0 + (1ull << 27);  // (a buffer of its own, past the C2 input)
+        p1.shift = 4;
+        p1.table = next;
+        p1.raw_table = 1;
+        p1.next_table = t2;
+        p1.zero_table = t3;
+        line("c2_keys_middle_pass_raw_offsets", n, 8, best_of(reps * 4, 3, [&] {
+                 rs_scatter_lines<4, 256, 16, kLineKeys, false, kDigitShift, 1><<<(unsigned)chunks, 256>>>(p1);
+             }));
+        // and with those offsets pre-scanned instead (the pass without raw_offsets, same input and tables)
+        CK(hipMemcpy(t3, next, 16 * chunks * 4, hipMemcpyDeviceToDevice));
+        ScanArgs sa{};
+        sa.table = t3;
+        sa.block_sums = bsums;
+        sa.m = 16 * chunks;
+        sa.nblocks = (uint32_t)((sa.m + kScanSegment - 1) / kScanSegment);
+        rs_scan_reduce<<<sa.nblocks, kScanThreads>>>(sa);
+        rs_scan_down<<<sa.nblocks, kScanThreads>>>(sa);
+        CK(hipDeviceSynchronize());
+        ScatterArgs p2 = p1;
+        p2.table = t3;
+        p2.raw_table = 0;
+        p2.zero_table = nullptr;
+        line("c2_keys_middle_pass_scanned", n, 8, best_of(reps * 4, 3, [&] {
+                 rs_scatter_lines<4, 256, 16, kLineKeys, false, kDigitShift, 1><<<(unsigned)chunks, 256>>>(p2);
+             }));
+#endif
     }
     return 0;
 }

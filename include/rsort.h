@@ -269,6 +269,12 @@ RSORT_API int rsort_partition_device(const uint32_t *d_keys_in, const uint32_t *
                                      const uint32_t *splitters, int num_buckets,
                                      uint32_t *d_bucket_starts, void *d_workspace,
                                      size_t workspace_bytes, void *stream);
+/* After rsort_partition_device(n, num_buckets, pairs) has completed on `stream` in `d_workspace`: its
+ * on-device self-check, as rsort_plan_check reports a sort's (bit 1: its scatter's rank check failed).
+ * Synchronises the stream. rsort_u32_multi* reads it after every partition and returns RSORT_ERR_CHECK
+ * on every rank when any rank's failed. */
+RSORT_API int rsort_partition_check(int64_t n, int num_buckets, int pairs, const void *d_workspace, int *flags,
+                                    void *stream);
 /* Histogram of the top `top_bits` (1..12) bits of n keys into d_hist[2^top_bits] (u32,
  * overwritten). Workspace: rsort_workspace_size(n, top_bits, 0). */
 RSORT_API int rsort_top_histogram(const uint32_t *d_keys, int64_t n, int top_bits,

@@ -104,3 +104,48 @@ def test_rank_check_clean_on_clustered_extremes():
             ko, _ = _sort(x, None, k, p, ws)
             assert rs.plan_check(p, ws) == 0
             assert np.array_equal(ko, np.sort(x))
+
+
+def test_partition_check_and_multi_gpu_sort_report_a_broken_lane_order():
+    """The multi-GPU partition (rsort_partition_device: the line kernel with splitter digits) runs the same
+    rank check; rsort_partition_check reads it, and rsort_u32_multi* turns a failure on any rank into
+    RSORT_ERR_CHECK on every rank before any key moves (loopback transport, 3 ranks on this card)."""
+    import sys
+    import threading
+    n = (1 << 22) + 17
+    x = uniform_keys(n, seed=5)
+    d = rs.from_numpy_u32(x)
+    out = rs.empty_u32(n)
+    spl = [1 << 30, 1 << 31, 3 << 30]
+    starts = torch.empty(len(spl) + 2, dtype=torch.int32, device="cuda")
+    ws = rs.workspace(int(rs._lib().rsort_partition_workspace_size(n, len(spl) + 1, 0)))
+    rs.partition_device(d, out, spl, starts, ws=ws)
+    assert rs.partition_check(n, len(spl) + 1, False, ws) == 0
+    with rs.rank_fault():
+        rs.partition_device(d, out, spl, starts, ws=ws)
+        assert rs.partition_check(n, len(spl) + 1, False, ws) & rs.CHECK_RANK_ORDER
+    world = 3
+    grp = rs.LoopbackGroup(world)
+    inputs = [rs.from_numpy_u32(uniform_keys(n, seed=50 + r)) for r in range(world)]
+    res = [None] * world
+
+    def run(r):
+        torch.cuda.set_device(0)
+        st = torch.cuda.Stream()
+        try:
+            with torch.cuda.stream(st):
+                rs.multi_sort_device(grp.transport(r), inputs[r], 8, capacity=world * n, stream=st)
+                st.synchronize()
+                res[r] = 0
+        except rs.RSortError as e:
+            res[r] = e.status
+
+    with rs.rank_fault():
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=240)
+    assert not any(t.is_alive() for t in th)
+    grp.close()
+    assert res == [11] * world, res
