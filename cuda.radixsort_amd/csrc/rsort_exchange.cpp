@@ -17,8 +17,7 @@
 namespace {
 
 constexpr int kMaxRanks = RSORT_MAX_RANKS;
-// world <= 8: 2 * (world - 1) <= 14 splitters, the partition's limit is 15 (16 buckets)
-constexpr int kMaxEqualRanks = 8;
+// every world: 2 * (world - 1) <= 30 splitters, within the partition's 31 (32 buckets)
 
 }  // namespace
 
@@ -65,39 +64,31 @@ int rsort_multi_splitters_make_hot(int world, const uint32_t *quantile_keys, con
     out->world = world;
     for (int i = 1; i + 1 < world; ++i)
         if (quantile_keys[i] < quantile_keys[i - 1]) return RSORT_ERR_ARG;
-    if (world <= kMaxEqualRanks) {
-        // A hot quantile key v (hot == nullptr: every one) gets its own bucket [v, v + 1) between the
-        // buckets below and above it, and the rank boundary cuts INSIDE it at the balancing position: a
-        // run of equal keys is split across ranks. A key that is not hot is a plain splitter: the ranks
-        // meet at v (its few copies all go up), one bucket fewer -- for distinct keys every quantile is
-        // plain, and the partition computes a digit from world - 1 splitters instead of 2 (world - 1)
-        // (2^30 keys into 8 ranks: 3.08 ms against 5.43 ms with 15 buckets, dev/part_lab.py). Equal
-        // consecutive quantile keys are one run: one bucket, hot.
-        // bucket j >= 1 is [split[j - 1], split[j]); the bucket starting at split[i] is bucket i + 1
-        int r = 1;
-        while (r < world) {
-            const uint32_t v = quantile_keys[r - 1];
-            int e = r + 1;  // boundaries r .. e - 1 share the key v
-            while (e < world && quantile_keys[e - 1] == v) ++e;
-            bool eq = hot == nullptr || e - r > 1;
-            for (int b = r; b < e && !eq; ++b) eq = hot[b - 1] != 0;
-            const int at = out->nsplit;
-            out->split[out->nsplit++] = v;
-            // key 0xFFFFFFFF: its bucket [v, v + 1) is everything from v on (no upper splitter, and the
-            // bucket above it does not exist)
-            if (eq && v != 0xFFFFFFFFu) out->split[out->nsplit++] = v + 1u;
-            for (int b = r; b < e; ++b) {
-                out->cut_bucket[b] = at + 1;
-                out->cut_inside[b] = eq ? 1 : 0;
-            }
-            r = e;
+    // A hot quantile key v (hot == nullptr: every one) gets its own bucket [v, v + 1) between the
+    // buckets below and above it, and the rank boundary cuts INSIDE it at the balancing position: a
+    // run of equal keys is split across ranks. A key that is not hot is a plain splitter: the ranks
+    // meet at v (its few copies all go up), one bucket fewer -- for distinct keys every quantile is
+    // plain, and the partition computes a digit from world - 1 splitters instead of 2 (world - 1)
+    // (2^30 keys into 8 ranks: 2.44 ms against 2.64 ms with 15 buckets, dev/part_lab.py). Equal
+    // consecutive quantile keys are one run: one bucket, hot.
+    // bucket j >= 1 is [split[j - 1], split[j]); the bucket starting at split[i] is bucket i + 1
+    int r = 1;
+    while (r < world) {
+        const uint32_t v = quantile_keys[r - 1];
+        int e = r + 1;  // boundaries r .. e - 1 share the key v
+        while (e < world && quantile_keys[e - 1] == v) ++e;
+        bool eq = hot == nullptr || e - r > 1;
+        for (int b = r; b < e && !eq; ++b) eq = hot[b - 1] != 0;
+        const int at = out->nsplit;
+        out->split[out->nsplit++] = v;
+        // key 0xFFFFFFFF: its bucket [v, v + 1) is everything from v on (no upper splitter, and the
+        // bucket above it does not exist)
+        if (eq && v != 0xFFFFFFFFu) out->split[out->nsplit++] = v + 1u;
+        for (int b = r; b < e; ++b) {
+            out->cut_bucket[b] = at + 1;
+            out->cut_inside[b] = eq ? 1 : 0;
         }
-    } else {
-        for (int r = 1; r < world; ++r) {
-            out->split[out->nsplit++] = quantile_keys[r - 1];
-            out->cut_bucket[r] = r;
-            out->cut_inside[r] = 0;
-        }
+        r = e;
     }
     return RSORT_OK;
 }

@@ -14,7 +14,7 @@ constexpr int kMaxBits = 13;            // the reference's SMEM limit (Parallel7
 constexpr int kScanThreads = 256;
 constexpr int kScanPerThread = 16;
 constexpr int kScanSegment = kScanThreads * kScanPerThread;  // table entries per scan block
-constexpr int kMaxSplitters = 15;          // partition: <= 16 buckets
+constexpr int kMaxSplitters = 31;          // partition: <= 32 buckets (2 x 16 ranks' equal-key splitters)
 
 enum DigitMode : int { kDigitShift = 0, kDigitSplit = 1 };
 

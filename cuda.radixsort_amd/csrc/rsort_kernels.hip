@@ -380,23 +380,73 @@ __device__ __forceinline__ uint32_t block_excl_scan1(uint32_t v, uint32_t *s_ws,
     return pre + inc - v;
 }
 
+// Split mode (partitions): the splitters are read from the kernel arguments once, at construction, into
+// wave-uniform registers, padded to 2^BITS - 1 with ~0u; cmp() is then a fixed run of compares and adds
+// clamped to nsplit (a padded ~0u only counts for key ~0u, where every real splitter counts too). An
+// early-exit loop over nsplit splitters instead compiled to a scalar loop re-reading the kernel arguments
+// for every key (16 buckets: 2.08 ms to count 2^30 keys, dev/LOG.md round 6).
+//
+// Prefix table (the partition's histogram and line scatter with > 8 buckets, kSplitTabWords of LDS): a
+// wave64 compare costs 4 cycles per SIMD, so 15 splitters took ~34 VALU cycles x 4 per key -- more than
+// the key's whole HBM time. The table holds, per 11-bit key prefix, the digit of the prefix's smallest
+// key (low 5 bits) and how many splitters lie inside the prefix's range (high 3 bits, mostly 0; 7: 7 or
+// more, up to the last); a key's digit is the entry's low bits plus the splitters from there on that it
+// reaches, compared against an LDS copy of the splitters after the entries.
+constexpr uint32_t kSplitTabBits = 11;
+constexpr uint32_t kSplitTabWords = (1u << kSplitTabBits) / 4 + 32;  // 2 KB of entries + 32 splitters
 template <int BITS, int DMODE>
 struct Digit {
+    // only 2^BITS - 1 splitters can exist (the host sizes BITS to the bucket count)
+    static constexpr int NS =
+        DMODE == kDigitShift ? 1 : (((1 << BITS) - 1) < kMaxSplitters ? ((1 << BITS) - 1) : kMaxSplitters);
     uint32_t shift;
     uint32_t nsplit;
-    const uint32_t *split;
+    uint32_t sp[NS];
+    uint32_t *tab;  // split mode: the prefix table in LDS (fill_table), or nullptr: compares only
+    __device__ __forceinline__ Digit(uint32_t shift_, uint32_t nsplit_, const uint32_t *split,
+                                     uint32_t *tab_ = nullptr)
+        : shift(shift_), nsplit(nsplit_), tab(tab_) {
+        if constexpr (DMODE == kDigitSplit) {
+#pragma unroll
+            for (int i = 0; i < NS; ++i) sp[i] = (uint32_t)i < nsplit_ ? split[i] : ~0u;
+        } else {
+            sp[0] = 0;
+        }
+    }
+    __device__ __forceinline__ uint32_t cmp(uint32_t key) const {
+        uint32_t d = 0;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) d += key >= sp[i] ? 1u : 0u;
+        return d < nsplit ? d : nsplit;
+    }
+    // the prefix table, by the workgroup's `threads` threads (the caller synchronises before use)
+    __device__ __forceinline__ void fill_table(uint32_t t, uint32_t threads) const {
+        if constexpr (DMODE == kDigitSplit) {
+            constexpr uint32_t SH = 32 - kSplitTabBits;
+            for (uint32_t wd = t; wd < (1u << kSplitTabBits) / 4; wd += threads) {
+                uint32_t v = 0;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint32_t p = wd * 4 + b;
+                    const uint32_t lo = cmp(p << SH), hi = cmp((p << SH) | ((1u << SH) - 1u));
+                    v |= (lo | min(hi - lo, 7u) << 5) << (8 * b);
+                }
+                tab[32 + wd] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < 32; ++i)  // (constant indices: sp stays in registers)
+                if (t == (uint32_t)i) tab[i] = i < NS ? sp[i < NS ? i : 0] : ~0u;
+        }
+    }
     __device__ __forceinline__ uint32_t operator()(uint32_t key) const {
         if constexpr (DMODE == kDigitShift) {
             return (key >> shift) & ((1u << BITS) - 1u);
         } else {
-            // only 2^BITS - 1 splitters can exist (the host sizes BITS to the bucket count)
-            constexpr int NS = ((1 << BITS) - 1) < kMaxSplitters ? ((1 << BITS) - 1) : kMaxSplitters;
-            uint32_t d = 0;
-#pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if ((uint32_t)i >= nsplit) break;  // uniform: a scalar branch, not per-lane selects
-                d += key >= split[i] ? 1u : 0u;
-            }
+            if (tab == nullptr) return cmp(key);
+            const uint32_t e = reinterpret_cast<const uint8_t *>(tab + 32)[key >> (32 - kSplitTabBits)];
+            uint32_t d = e & 31u;
+            const uint32_t span = e >> 5, end = span == 7u ? nsplit : d + span;
+            while (d < end && key >= tab[d]) ++d;  // (non-decreasing splitters: the first one above the key)
             return d;
         }
     }
@@ -591,6 +641,85 @@ __device__ __forceinline__ void hist_joint_body(const HistArgs &a, uint32_t *s_j
     RS_WG_TH1;
 }
 
+// Partitions into <= 8 buckets (split digits, BITS <= 3): per lane, in registers, the count of keys >=
+// each splitter -- 7 compares and adds per key -- and no LDS add per key (with two or four buckets 32 or
+// 16 lanes of every add met on one LDS counter). Bucket b holds ge[b - 1] - ge[b] keys (non-decreasing
+// splitters; ge[-1] = every key counted, ge[nsplit] = 0). More buckets (BITS = 4) count their digits
+// from the prefix table (Digit::fill_table) into the LDS counters like shift digits.
+template <int BITS, int THREADS, int NT>
+__device__ __forceinline__ void hist_split_body(const HistArgs &a, uint32_t *s_h, uint32_t c, uint32_t sub,
+                                                uint32_t S) {
+    typedef Digit<BITS, kDigitSplit> D;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int NS = D::NS;
+    constexpr uint32_t R = 1u << BITS;
+    const uint32_t t = threadIdx.x;
+    const D dig{a.shift, a.nsplit, a.splitters};
+    uint32_t ge[NS + 1];  // ge[NS]: the keys counted
+#pragma unroll
+    for (int i = 0; i <= NS; ++i) ge[i] = 0u;
+    auto cnt = [&](uint32_t x) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) ge[i] += x >= dig.sp[i] ? 1u : 0u;
+        ge[NS] += 1u;
+    };
+    const uint64_t cbeg = (uint64_t)c * a.chunk_keys;
+    const uint64_t cend = min(cbeg + a.chunk_keys, a.n);
+    const uint64_t part = (((cend > cbeg ? cend - cbeg : 0) + S - 1) / S + 3) & ~(uint64_t)3;
+    const uint64_t beg = min(cbeg + sub * part, cend);
+    const uint64_t end = min(beg + part, cend);
+    uint64_t tail = beg;
+    if (a.vec) {
+        const uint64_t vb = min((beg + 3) & ~(uint64_t)3, end);
+        for (uint64_t i = beg + t; i < vb; i += THREADS) cnt(a.keys[i]);
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(a.keys + vb);
+        const uint32_t nvec = (uint32_t)((end - vb) / 4);
+        constexpr int U = 4;
+        for (uint32_t v0 = t; v0 < nvec; v0 += THREADS * U) {
+            u32x4 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = v0 + u * THREADS;
+                q[u] = v < nvec ? (NT ? __builtin_nontemporal_load(p + v) : p[v]) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (v0 + u * THREADS < nvec) {
+                    cnt(q[u].x);
+                    cnt(q[u].y);
+                    cnt(q[u].z);
+                    cnt(q[u].w);
+                }
+            }
+        }
+        tail = vb + (uint64_t)nvec * 4;
+    }
+    for (uint64_t i = tail + t; i < end; i += THREADS) cnt(a.keys[i]);
+    // wave sums -> LDS -> bucket counts
+    const uint32_t w = t / kWave;
+#pragma unroll
+    for (int i = 0; i <= NS; ++i) {
+        uint32_t v = ge[i];
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane_id() == 0) s_h[w * (NS + 1) + i] = v;
+    }
+    __syncthreads();
+    auto total = [&](uint32_t j) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int x = 0; x < THREADS / kWave; ++x) s += s_h[x * (NS + 1) + j];
+        return s;
+    };
+    const uint32_t ns = a.nsplit;
+    for (uint32_t d = t; d < R; d += THREADS) {
+        const uint32_t hi = d == 0u ? total(NS) : (d <= ns ? total(d - 1u) : 0u);
+        const uint32_t v = d < ns ? hi - total(d) : hi;
+        if (S == 1) a.table[(uint64_t)d * a.num_chunks + c] = v;
+        else if (v) atomicAdd(&a.table[(uint64_t)d * a.num_chunks + c], v);
+    }
+}
+
 template <int BITS, int THREADS, int DMODE, int NT = 0, int SUB = 1, bool JOINT = false>
 __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     constexpr uint32_t R = 1u << BITS;
@@ -629,12 +758,20 @@ __global__ __launch_bounds__(THREADS) void rs_histogram(HistArgs a) {
     // raw-table plans (HistArgs::zero): clear the next table on the way
     for (uint64_t i = (uint64_t)blockIdx.x * THREADS + t; i < a.zero_n; i += (uint64_t)gridDim.x * THREADS)
         a.zero[i] = 0u;
+    constexpr bool SPLIT_TAB = DMODE == kDigitSplit && BITS > 3;
+    if constexpr (DMODE == kDigitSplit && !SPLIT_TAB) {
+        static_assert(W * (Digit<BITS, DMODE>::NS + 1) <= (int)PLAIN, "the wave sums fit s_h");
+        hist_split_body<BITS, THREADS, NT>(a, s_h, c, sub, S);
+        return;
+    }
+    __shared__ uint32_t s_stab[SPLIT_TAB ? kSplitTabWords : 1];
     for (uint32_t i = t; i < HW * R * SB; i += THREADS) s_h[i] = 0;
+    const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters, SPLIT_TAB ? s_stab : nullptr};
+    if constexpr (SPLIT_TAB) dig.fill_table(t, THREADS);
     __syncthreads();
 
     // counter of digit d: my[d * SB] (this lane's sub-counter)
     uint32_t *my = s_h + (HW > 1 ? (t / kWave) * R * SB : 0) + (SB > 1 ? lane_id() % SB : 0);
-    const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
     // keys [beg, end) into the LDS counters (16-B loads from the first 16-B aligned key on)
     auto count_range = [&](uint64_t beg, uint64_t end) {
         uint64_t tail = beg;
@@ -1776,7 +1913,12 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
     const uint32_t w = t / kWave;
     const uint32_t lane = lane_id();
     const uint32_t c = blockIdx.x;
-    const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters};
+    // 16-bucket split digits from the prefix table (Digit::fill_table; built before the first tile's
+    // ranking). With <= 7 splitters the compares are cheaper than the table's LDS read (2^30 keys into 8
+    // buckets: 1.79 ms with compares, 1.83 with the table; into 16: 2.25 with compares, 1.74 with it)
+    constexpr bool STAB = DMODE == kDigitSplit && BITS > 3;
+    __shared__ uint32_t s_stab[STAB ? kSplitTabWords : 1];
+    const Digit<BITS, DMODE> dig{a.shift, a.nsplit, a.splitters, STAB ? s_stab : nullptr};
     uint64_t cbeg = (uint64_t)c * a.chunk_keys;
     uint64_t cend = min(cbeg + a.chunk_keys, a.n);
     uint32_t head = 0;  // leading keys of the first tile that belong to the previous chunk
@@ -1827,6 +1969,10 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
     uint32_t key[KPT];
     uint32_t val[PAIRS ? KPT : 1];
     if (cbeg < cend) load_tile(cbeg, key, val);
+    if constexpr (STAB) {
+        dig.fill_table(t, THREADS);  // (while the first tile's loads are in flight)
+        __syncthreads();
+    }
     if constexpr (NX) {
         // this workgroup's share of the table the pass after next counts into (nobody reads that
         // one in this pass) is cleared on the way
@@ -2704,7 +2850,7 @@ static void *reg_scatter() {
 template <int BITS>
 static hipError_t hist_bits(int dmode, const HistArgs &a, hipStream_t s) {
     if (dmode == kDigitSplit) {
-        if constexpr (BITS <= 4) {
+        if constexpr (BITS <= 5) {
             rs_histogram<BITS, kHistThreads, kDigitSplit, 1, 8><<<a.num_chunks * a.split, kHistThreads, 0, s>>>(a);
             return hipGetLastError();
         }
@@ -2745,9 +2891,9 @@ template <int BITS, bool PAIRS>
 static void *scatter_pick2(int rank, int dmode, int geom, int aligned16) {
     if (rank != kRankSplit && rank != kRankAtomic && rank != kRankCount) return nullptr;
     if (dmode == kDigitSplit) {
-        if constexpr (BITS <= 4) {
+        if constexpr (BITS <= 5) {
             if constexpr (BITS >= 2) {
-                // partition into 3..16 key ranges: whole lines from 4096-key tiles, like k = 3, 4
+                // partition into 3..32 key ranges: whole lines from 4096-key tiles, like k = 3, 4
                 // (a digit's thread group must fit one wave: BITS >= 2)
                 constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
                 if (geom == kGeomSmall && rank == kRankAtomic && aligned16)

@@ -7,7 +7,7 @@ rsort_multi_splitters_make, rsort_multi_exchange_plan), so both paths split and 
 
   1. all_gather of the key counts                      -> the sampling plan (one stride for all)
   2. a regular sample of the local keys (HIP), all_gather, sort (HIP) -> world-1 quantile KEYS
-  3. splitters with an equal-keys bucket per hot quantile key (world <= 8): a run of equal keys --
+  3. splitters with an equal-keys bucket per hot quantile key: a run of equal keys --
      a hot key, duplicate-heavy input -- is split across ranks in (source rank, position) order
   4. stable partition into those buckets (HIP: rsort_partition_device)
   5. all_gather of the bucket counts and capacities    -> the exchange plan, the same on every

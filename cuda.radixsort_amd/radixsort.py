@@ -573,7 +573,7 @@ def multi_sort_device(comm, keys, k_bits=8, vals=None, capacity=None, stream=Non
 
 
 MULTI_OVERLAP, MULTI_FULL, MULTI_NO_OVERLAP = 1, 2, 4
-MULTI_AUTO_OVERLAP_MAX_WORLD = 4  # neither overlap flag: the overlap runs for 2 <= world <= this (rsort.h)
+MULTI_AUTO_OVERLAP_MAX_WORLD = 8  # neither overlap flag: the overlap runs for 2 <= world <= this (rsort.h)
 
 
 def set_multi_options(flags: int) -> int:

@@ -6,7 +6,7 @@ each uncontended, at N = 2, 4, 8:
   plan        the sample / splitter phase of the whole protocol at one rank (loopback transport,
               RSORT_MULTI_FULL, rsort_multi_last_stats), plus a modelled RCCL latency per all-gather
   partition   rsort_partition_device into the buckets rsort_multi_splitters_make gives for N ranks
-              (N - 1 quantile keys, every one with its equal-keys bucket: 2N - 1 buckets)
+              (N - 1 quantile keys of distinct keys, none hot: N buckets)
   local sort  the sort of what one rank receives: 2^30 keys inside one rank's key range (the arrival
               of N sources; uniform keys: their top log2 N bits are the rank's)
   exchange    modelled: (N - 1) / N of the rank's keys, n / N per peer, each pair of GPUs on its own

@@ -34,6 +34,11 @@ def main():
         q = [(i << 32) // W for i in range(1, W)]
         cases[f"equal_buckets_w{W}"] = rs.multi_splitters(W, q).splitters
         cases[f"plain_w{W}"] = q
+    cases["plain_w16"] = [(i << 32) // 16 for i in range(1, 16)]  # the overlap's 2N buckets at N = 8
+    cases["equal_buckets_w16"] = rs.multi_splitters(16, cases["plain_w16"]).splitters  # every quantile hot: 31
+    # unequal buckets: the chunks' output offsets inside a bucket are then no power-of-two stride apart
+    cases["uneven_w2"] = [0x55555555]
+    cases["uneven_w4"] = [0x30000000, 0x70000000, 0xB0000000]
     cases["one_bucket"] = []
     res = {}
     for name, spl in cases.items():

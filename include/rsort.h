@@ -259,7 +259,7 @@ RSORT_API int rsort_profile_begin(void);
 RSORT_API int rsort_profile_end(rsort_phase_times *out);
 
 /* ---------------------------------------------------------------- multi-GPU building blocks */
-/* Stable partition of n keys (and values) into num_buckets (<= 16) key ranges:
+/* Stable partition of n keys (and values) into num_buckets (<= 32) key ranges:
  * bucket(key) = #{i : key >= splitters[i]} for the num_buckets-1 ascending host-side
  * splitters. Output is bucket-major and stable; d_bucket_starts[num_buckets + 1] receives
  * the exclusive bucket offsets (last = n). Workspace: rsort_partition_workspace_size. */
@@ -315,13 +315,12 @@ RSORT_API int rsort_sample_device(const uint32_t *d_keys, int64_t n, int64_t str
 RSORT_API int64_t rsort_multi_quantile_index(const rsort_sample_plan *sp, int i);
 
 /* 2. Splitters. From the world - 1 quantile keys v_1 <= ... <= v_{world-1}: the partition's
- * splitters and, for each rank boundary, where it cuts. For world <= 8 every distinct v gets a
- * bucket of its own, [v, v + 1) ("equal keys"), between the buckets of the keys below and above
- * it, and boundary r cuts INSIDE the equal-keys bucket of v_r at the position that balances the
- * ranks: a run of equal keys (a hot key, duplicate-heavy input) is split across ranks in global
- * (source rank, position) order, which keeps the sort stable. For world > 8 the 2 * (world - 1)
- * splitters would exceed the partition's 16 buckets: the splitters are the v's themselves and
- * boundaries cut on bucket edges. */
+ * splitters and, for each rank boundary, where it cuts. Every distinct v gets a bucket of its own,
+ * [v, v + 1) ("equal keys"), between the buckets of the keys below and above it, and boundary r
+ * cuts INSIDE the equal-keys bucket of v_r at the position that balances the ranks: a run of equal
+ * keys (a hot key, duplicate-heavy input) is split across ranks in global (source rank, position)
+ * order, which keeps the sort stable. (2 * (world - 1) <= 30 splitters: within the partition's 32
+ * buckets at every world size.) */
 typedef struct rsort_multi_splitters {
     int32_t world;
     int32_t nsplit;                                 /* partition splitters (buckets = nsplit + 1) */
@@ -374,7 +373,7 @@ RSORT_API int rsort_multi_exchange_rounds(int64_t max_message, int64_t limit, in
  * ranks' outputs in rank order gives Baseline1's result; pairs stay stable (equal keys keep their
  * (source rank, position) order). Steps: all-gather of the key counts -> a regular sample of the
  * keys, all-gathered and sorted on the device -> world - 1 quantile keys -> splitters with a
- * bucket of its own for each quantile key (world <= 8), so a run of equal keys is split across
+ * bucket of its own for each hot quantile key, so a run of equal keys is split across
  * ranks -> stable partition -> all-gather of the bucket counts and capacities -> the exchange
  * plan (the same on every rank) -> one exchange (own range by a device copy, the rest point to
  * point in rounds of <= 2^28 keys per message) -> local LSD sort. Synchronises `stream` four
@@ -422,16 +421,17 @@ RSORT_API int rsort_set_comm_timeout(int timeout_ms);
  *                       exchanged first, and each rank sorts its lower half on a second stream
  *                       while the upper halves are exchanged; same output.
  *  RSORT_MULTI_NO_OVERLAP  never cut the ranges in two.
- *  Neither: the overlap runs for 2 <= world <= 4 (RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD) and not above, where
- *                       its 2 x world buckets make the partition cost more than the half sort it hides
- *                       (measured on one GPU, partition 5.4 vs 3.1 ms at world 8).
+ *  Neither: the overlap runs for 2 <= world <= 8 (RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD; 2 x world <=
+ *                       RSORT_MAX_RANKS virtual ranks), where it is predicted faster at every size
+ *                       (components measured on one GPU; at world 8 the partition into
+ *                       16 buckets costs 2.40 ms against 2.49 ms for 8).
  *  RSORT_MULTI_FULL     run the whole protocol also at world 1 (sample, partition into one
  *                       bucket, self exchange): for tests and overhead measurements. By default
  *                       one rank sorts its keys directly (the partition would be a copy). */
 #define RSORT_MULTI_OVERLAP 1
 #define RSORT_MULTI_FULL 2
 #define RSORT_MULTI_NO_OVERLAP 4
-#define RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD 4
+#define RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD 8
 RSORT_API int rsort_set_multi_options(int flags);
 
 /* Per-phase record of a multi-GPU sort (rsort_u32_multi*), for the N-GPU bench line. Off by

@@ -68,7 +68,7 @@ int main(int argc, char **argv) {
         for (int i = 1; i < sp.nsplit; ++i)
             if (sp.split[i] < sp.split[i - 1]) FAIL("splitters not monotone");
         const int buckets = sp.nsplit + 1;
-        if (buckets > 16) FAIL("more than 16 buckets (%d)", buckets);
+        if (buckets > 32) FAIL("more than 32 buckets (%d)", buckets);
         // bucket counts per source rank
         std::vector<int64_t> counts((size_t)world * buckets), n(world, 0);
         const int cmode = (int)(next() % 4);

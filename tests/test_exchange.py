@@ -95,8 +95,9 @@ def test_splitters_equal_key_buckets():
     spl = rs.multi_splitters(3, [5, 0xFFFFFFFF])  # no bucket above the largest key
     assert spl.splitters == [5, 6, 0xFFFFFFFF]
     assert list(spl.cut_bucket)[1:3] == [1, 3]
-    spl = rs.multi_splitters(12, list(range(100, 1200, 100)))  # world > 8: bucket edges
-    assert spl.splitters == list(range(100, 1200, 100)) and not any(list(spl.cut_inside)[1:12])
+    spl = rs.multi_splitters(16, list(range(100, 1600, 100)))  # every world: 2 x 15 = 30 splitters (<= 31)
+    assert spl.splitters == sum(([v, v + 1] for v in range(100, 1600, 100)), [])
+    assert list(spl.cut_bucket)[1:16] == list(range(1, 30, 2)) and all(list(spl.cut_inside)[1:16])
     assert rs.multi_splitters(1, []).nsplit == 0
     with pytest.raises(rs.RSortError):
         rs.multi_splitters(3, [5, 4])  # not sorted

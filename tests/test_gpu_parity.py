@@ -395,7 +395,7 @@ def test_top_histogram_sampled(n, stride, bits):
     assert np.array_equal(host(h), np.bincount(sample >> np.uint32(32 - bits), minlength=1 << bits).astype(np.uint32))
 
 
-@pytest.mark.parametrize("nb", [1, 2, 3, 8, 16])
+@pytest.mark.parametrize("nb", [1, 2, 3, 8, 16, 17, 32])
 def test_partition_stable(nb):
     n = 200003
     x = zipf_keys(n, seed=nb)
@@ -417,7 +417,7 @@ def _cus():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
-@pytest.mark.parametrize("nb,repeat", [(2, False), (8, True), (15, True), (16, False)])
+@pytest.mark.parametrize("nb,repeat", [(2, False), (8, True), (15, True), (16, False), (31, True), (32, False)])
 def test_partition_stable_large(nb, repeat):
     """keys-only partitions of n >= 2 x CUs x 8192 keys run the 512 x 16 line tiles with
     splitter digits (rsort_capi.cpp choose_geom). n = 2 x CUs x 8192 + odd, Zipf keys; with
@@ -426,7 +426,7 @@ def test_partition_stable_large(nb, repeat):
     starts."""
     n = 2 * _cus() * 8192 + 4099
     x = zipf_keys(n, seed=nb + 100)
-    q = np.unique(x[:: max(1, n // 64)])
+    q = np.unique(x[:: max(1, n // 512)])
     rng = np.random.default_rng(nb)
     if repeat:
         vs = [int(v) for v in np.sort(rng.choice(q, size=nb // 2, replace=False))]
@@ -442,6 +442,62 @@ def test_partition_stable_large(nb, repeat):
     starts = rs.empty_u32(nb + 1)
     rs.partition_device(dev(x), ko, split.tolist(), starts)
     torch.cuda.synchronize()
+    assert np.array_equal(host(ko), x[order])
+    exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
+    assert np.array_equal(host(starts), exp)
+
+
+def _prefix_table_case(case, rng):
+    """Splitters that stress the partition kernels' split digits (Digit: an 11-bit prefix table, then
+    compares against the splitters inside the key's prefix range): every splitter inside one prefix,
+    the extreme values, repeated splitters."""
+    if case in ("one_prefix", "one_prefix31"):  # 15 (31) splitters, 16 (32) buckets, in one 2^21-key prefix
+        base = 0x2A5 << 21
+        m = 31 if case == "one_prefix31" else 15
+        return np.sort(base + rng.choice(1 << 21, size=m, replace=False)).astype(np.uint32)
+    if case == "many31":  # 32 buckets: 31 random splitters, 4 of them in one prefix
+        v = rng.integers(0, 1 << 32, size=27, dtype=np.uint64).tolist() + [(0x123 << 21) + i for i in (0, 5, 9, 77)]
+        return np.sort(np.array(v, np.uint64)).astype(np.uint32)
+    if case == "edges":  # 0, 1, prefix boundaries and ~0u
+        v = [0, 1, (1 << 21) - 1, 1 << 21, 0x7FFFFFFF, 0x80000000, 0xFFE00000, 0xFFFFFFFE, 0xFFFFFFFF]
+        v += [int(x) for x in rng.integers(0, 1 << 32, size=6, dtype=np.uint64)]
+        return np.sort(np.array(v, np.uint64)).astype(np.uint32)
+    # repeated splitters, 8 buckets (empty ones between the repeats)
+    s = int(rng.integers(1 << 20, 1 << 31))
+    return np.array([s, s, s, s + 1, s + 1, s + (1 << 21), 0xFFFFFFFF], np.uint32)
+
+
+@pytest.mark.parametrize("case", ["one_prefix", "one_prefix31", "many31", "edges", "dups"])
+@pytest.mark.parametrize("size", ["small", "large", "pairs"])
+def test_partition_prefix_table(case, size):
+    """Partitions whose keys sit on and next to every splitter and every prefix boundary near one, in
+    all three split-digit kernels (histogram, 4096-key and 8192-key line tiles; pairs), against numpy's
+    stable argsort of searchsorted(side='right') buckets and the bucket starts."""
+    rng = np.random.default_rng(len(case) * 7 + len(size))
+    split = _prefix_table_case(case, rng)
+    nb = split.size + 1
+    n = 2 * _cus() * 8192 + 4099 if size == "large" else 150001
+    near = []
+    for s in split.astype(np.int64):
+        p = (s >> 21) << 21
+        near += [s - 1, s, s + 1, p - 1, p, p + (1 << 21) - 1, p + (1 << 21)]
+    near = np.array([x for x in near if 0 <= x <= 0xFFFFFFFF], np.uint64).astype(np.uint32)
+    x = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    pos = rng.choice(n, size=n // 2, replace=False)
+    x[pos] = near[rng.integers(0, near.size, size=pos.size)]
+    bucket = np.searchsorted(split, x, side="right")
+    order = np.argsort(bucket, kind="stable")
+    ko = rs.empty_u32(n)
+    starts = rs.empty_u32(nb + 1)
+    if size == "pairs":
+        v = np.arange(n, dtype=np.uint32)
+        vo = rs.empty_u32(n)
+        rs.partition_device(dev(x), ko, split.tolist(), starts, vals_in=dev(v), vals_out=vo)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(vo), v[order])
+    else:
+        rs.partition_device(dev(x), ko, split.tolist(), starts)
+        torch.cuda.synchronize()
     assert np.array_equal(host(ko), x[order])
     exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
     assert np.array_equal(host(starts), exp)

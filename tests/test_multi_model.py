@@ -47,14 +47,13 @@ def test_prediction_by_hand(bench, model):
 
 
 def test_prediction_orders(bench, model):
-    """Slower links predict slower steps; the automatic overlap (2 <= N <= 4, rsort.h) predicts faster steps
-    where it runs and slower ones at N = 8, where it does not."""
+    """Slower links predict slower steps; the automatic overlap (2 <= N <= 8, rsort.h) predicts faster steps
+    at every N it runs at, on both link rates."""
     for w in (2, 4, 8):
         for h in (1, 2):
             assert bench.predict_multi_step(model, w, h, 64.0) > bench.predict_multi_step(model, w, h, 153.0)
-    for w in (2, 4):
-        assert bench.predict_multi_step(model, w, 2, 153.0) < bench.predict_multi_step(model, w, 1, 153.0)
-    assert bench.predict_multi_step(model, 8, 2, 153.0) > bench.predict_multi_step(model, 8, 1, 153.0)
-    main, detail = bench.multi_prediction(8, 1)
-    assert main == pytest.approx(bench.predict_multi_step(model, 8, 1, 153.0), abs=1e-3)
-    assert detail["halves"] == 1 and detail["link_64GBs_ms"] > main
+        for link in (64.0, 153.0):
+            assert bench.predict_multi_step(model, w, 2, link) < bench.predict_multi_step(model, w, 1, link)
+    main, detail = bench.multi_prediction(8, 2)
+    assert main == pytest.approx(bench.predict_multi_step(model, 8, 2, 153.0), abs=1e-3)
+    assert detail["halves"] == 2 and detail["link_64GBs_ms"] > main
