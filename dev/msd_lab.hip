@@ -1,0 +1,208 @@
+// Lab (round 6): the last phase of an MSD + in-LDS hybrid for C3 (2^30 keys, k = 8). Two MSD passes by the
+// top two bytes would leave 65536 buckets of ~16K keys, contiguous; this kernel then sorts each bucket by
+// its low 16 bits inside LDS (two 8-bit counting passes, lane-ordered ranks) and writes it once: one read and
+// one write of the keys for the last two digits, where LSD passes 0 and 1 read and write them twice.
+// Measured here on synthetic bucketed input (bucket b = keys with top 16 bits b, low 16 bits random):
+// the time of this phase decides whether the hybrid (histogram + 2 MSD passes + this) beats 4 LSD passes.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I cuda.radixsort_amd/csrc dev/msd_lab.hip -o dev/msd_lab
+//   dev/msd_lab [reps = 10]   (JSON lines)
+#include "../cuda.radixsort_amd/csrc/rsort_kernels.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+using namespace rsort;
+
+#define CK(x)                                                                     \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            printf("HIP error %s at line %d\n", hipGetErrorString(e_), __LINE__); \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+// one workgroup per bucket (grid-stride); a bucket of n <= THREADS * KPT keys
+template <int THREADS, int KPT>
+__global__ __launch_bounds__(THREADS, 1) void bucket_sort16(const uint32_t *in, uint32_t *out, const uint32_t *starts,
+                                                             uint32_t nb, uint32_t *err) {
+    constexpr int W = THREADS / kWave;
+    constexpr uint32_t SEG = kWave * KPT;
+    constexpr uint32_t CAP = THREADS * KPT;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) uint32_t X[CAP + 4];
+    __shared__ uint32_t cnt[W * 256];
+    __shared__ uint32_t s_ws[W];
+    const uint32_t t = threadIdx.x, w = t / kWave, lane = lane_id();
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t s = starts[b], n = starts[b + 1] - s;
+        if (n > CAP) {
+            if (t == 0) atomicAdd(err, 1u);
+            continue;
+        }
+        const uint32_t a = s & 3u;  // X[a + i] holds key i at the end: quads of X are 16-B aligned in `out`
+        uint32_t key[KPT];
+        const uint32_t base_i = w * SEG + lane;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t i = base_i + j * kWave;
+            key[j] = i < n ? in[s + i] : 0u;
+        }
+        for (int pass = 0; pass < 2; ++pass) {
+            const uint32_t sh = pass * 8;
+            for (uint32_t i = lane; i < 256; i += kWave) cnt[w * 256 + i] = 0;  // (own wave's row)
+            uint32_t rk[KPT];
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t i = base_i + j * kWave;
+                const uint32_t d = (key[j] >> sh) & 255u;
+                // whole-wave slot: every key valid (rank_add, aggregated); else masked lane-ordered adds
+                if (w * SEG + (j + 1) * kWave <= n) rk[j] = rank_add(&cnt[w * 256], d);
+                else rk[j] = i < n ? atomicAdd(&cnt[w * 256 + d], 1u) : 0u;
+            }
+            __syncthreads();
+            // per digit: exclusive prefix over waves (in place), total; then over digits
+            uint32_t tot = 0;
+            if (t < 256) {
+#pragma unroll
+                for (int x = 0; x < W; ++x) {
+                    const uint32_t c = cnt[x * 256 + t];
+                    cnt[x * 256 + t] = tot;
+                    tot += c;
+                }
+            }
+            uint32_t all;
+            const uint32_t dbase = block_excl_scan<THREADS>(t < 256 ? tot : 0u, s_ws, all);
+            if (t < 256) {
+#pragma unroll
+                for (int x = 0; x < W; ++x) cnt[x * 256 + t] += dbase;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t i = base_i + j * kWave;
+                if (i < n) X[a + cnt[w * 256 + ((key[j] >> sh) & 255u)] + rk[j]] = key[j];
+            }
+            __syncthreads();
+            if (pass == 0) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = base_i + j * kWave;
+                    key[j] = i < n ? X[a + i] : 0u;
+                }
+                __syncthreads();
+            }
+        }
+        // out[s - a + 4q .. + 3] = X[4q .. + 3], the slots before a and from a + n masked
+        uint32_t *o = out + (s - a);
+        const uint32_t nq = (a + n + 3) / 4;
+        for (uint32_t q = t; q < nq; q += THREADS) {
+            const u32x4 v = *reinterpret_cast<const u32x4 *>(&X[4 * q]);
+            if (4 * q >= a && 4 * q + 4 <= a + n) {
+                *reinterpret_cast<u32x4 *>(o + 4 * q) = v;
+            } else {
+#pragma unroll
+                for (uint32_t x = 0; x < 4; ++x)
+                    if (4 * q + x >= a && 4 * q + x < a + n) o[4 * q + x] = v[x];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// keys of bucket b = b << 16 | random low 16 bits; bucket sizes from `starts`
+__global__ void gen_bucketed(uint32_t *k, const uint32_t *starts, uint32_t nb, uint64_t seed) {
+    const uint32_t b = blockIdx.x;
+    if (b >= nb) return;
+    for (uint32_t i = starts[b] + threadIdx.x; i < starts[b + 1]; i += blockDim.x) {
+        uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ull;
+        z ^= z >> 29;
+        k[i] = (b << 16) | (uint32_t)(z & 0xFFFFu);
+    }
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 10;
+    const uint64_t N = 1ull << 30;
+    const uint32_t NB = 65536;
+    // bucket sizes: uniform keys' multinomial counts (mean 16384) from a host generator
+    std::vector<uint32_t> starts(NB + 1);
+    {
+        uint64_t x = 12345;
+        std::vector<uint64_t> sz(NB);
+        uint64_t tot = 0;
+        for (uint32_t b = 0; b < NB; ++b) {
+            // mean 16384, sd 128: sum of 16 uniforms approximates a normal
+            double u = 0;
+            for (int i = 0; i < 16; ++i) {
+                x = x * 6364136223846793005ull + 1442695040888963407ull;
+                u += (double)(x >> 11) / 9007199254740992.0;
+            }
+            sz[b] = (uint64_t)(16384.0 + (u - 8.0) * 128.0 / 1.1547);
+            tot += sz[b];
+        }
+        // fix the total to N
+        int64_t diff = (int64_t)N - (int64_t)tot;
+        for (uint32_t b = 0; diff != 0; b = (b + 1) % NB) {
+            if (diff > 0) { ++sz[b]; --diff; } else if (sz[b] > 0) { --sz[b]; ++diff; }
+        }
+        starts[0] = 0;
+        for (uint32_t b = 0; b < NB; ++b) starts[b + 1] = starts[b] + (uint32_t)sz[b];
+        uint64_t mx = *std::max_element(sz.begin(), sz.end());
+        printf("{\"buckets\": %u, \"max_bucket\": %llu}\n", NB, (unsigned long long)mx);
+    }
+    uint32_t *k0, *k1, *st, *err;
+    CK(hipMalloc(&k0, N * 4));
+    CK(hipMalloc(&k1, N * 4));
+    CK(hipMalloc(&st, (NB + 1) * 4));
+    CK(hipMalloc(&err, 4));
+    CK(hipMemset(err, 0, 4));
+    CK(hipMemcpy(st, starts.data(), (NB + 1) * 4, hipMemcpyHostToDevice));
+    gen_bucketed<<<NB, 256>>>(k0, st, NB, 77);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    struct V { const char *name; void (*fn)(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *); };
+    const V vars[] = {{"1024x20", bucket_sort16<1024, 20>}, {"1024x18", bucket_sort16<1024, 18>}};
+    for (const V &v : vars)
+    for (int grid : {256, 512}) {
+        auto run = [&](int g) { v.fn<<<g, 1024>>>(k0, k1, st, NB, err); };
+        run(grid);
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int r = 0; r < 3; ++r) {
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < reps; ++i) run(grid);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = std::min(best, ms / reps);
+        }
+        printf("{\"kernel\": \"bucket_sort16 %s\", \"grid\": %d, \"ms\": %.4f, \"frac_of_8TBs\": %.4f}\n", v.name, grid, best,
+               8.0 * N / (best * 1e-3) / 8e12);
+        fflush(stdout);
+    }
+    // check: every bucket sorted and a permutation of its input (sampled buckets, host)
+    uint32_t herr = 0;
+    CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> hin(N / 64), hout(N / 64);  // the first 1/64 of the keys (whole buckets)
+    CK(hipMemcpy(hin.data(), k0, hin.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hout.data(), k1, hout.size() * 4, hipMemcpyDeviceToHost));
+    uint64_t bad = 0, checked = 0;
+    for (uint32_t b = 0; b < NB && starts[b + 1] <= hin.size(); ++b) {
+        std::vector<uint32_t> x(hin.begin() + starts[b], hin.begin() + starts[b + 1]);
+        std::sort(x.begin(), x.end());
+        for (uint32_t i = starts[b]; i < starts[b + 1]; ++i) bad += x[i - starts[b]] != hout[i];
+        ++checked;
+    }
+    printf("{\"check\": \"%s\", \"buckets_checked\": %llu, \"mismatches\": %llu, \"oversized\": %u}\n",
+           bad == 0 && herr == 0 ? "ok" : "FAIL", (unsigned long long)checked, (unsigned long long)bad, herr);
+    return bad == 0 && herr == 0 ? 0 : 1;
+}
