@@ -28,7 +28,7 @@ using namespace rsort;
 
 // one workgroup per bucket (grid-stride); a bucket of n <= THREADS * KPT keys
 template <int THREADS, int KPT>
-__global__ __launch_bounds__(THREADS, 1) void bucket_sort16(const uint32_t *in, uint32_t *out, const uint32_t *starts,
+__global__ __launch_bounds__(THREADS, THREADS == 512 ? 2 : 1) void bucket_sort16(const uint32_t *in, uint32_t *out, const uint32_t *starts,
                                                              uint32_t nb, uint32_t *err) {
     constexpr int W = THREADS / kWave;
     constexpr uint32_t SEG = kWave * KPT;
@@ -169,10 +169,12 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     struct V { const char *name; void (*fn)(const uint32_t *, uint32_t *, const uint32_t *, uint32_t, uint32_t *); };
-    const V vars[] = {{"1024x20", bucket_sort16<1024, 20>}, {"1024x18", bucket_sort16<1024, 18>}};
+    const V vars[] = {{"1024x20", bucket_sort16<1024, 20>}, {"1024x18", bucket_sort16<1024, 18>},
+                      {"512x35", bucket_sort16<512, 35>}, {"512x34", bucket_sort16<512, 34>}};
     for (const V &v : vars)
-    for (int grid : {256, 512}) {
-        auto run = [&](int g) { v.fn<<<g, 1024>>>(k0, k1, st, NB, err); };
+    for (int grid : {256, 512, 1024}) {
+        const int th = v.name[0] == '5' ? 512 : 1024;
+        auto run = [&](int g) { v.fn<<<g, th>>>(k0, k1, st, NB, err); };
         run(grid);
         CK(hipDeviceSynchronize());
         float best = 1e30f;
