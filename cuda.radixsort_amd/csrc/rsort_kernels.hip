@@ -41,6 +41,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rsort_hooks.hpp"
@@ -1889,7 +1890,10 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
     // and write rows sub * WPT + i of their digit's column, which R apart share one bank
     constexpr uint32_t RS = counter_stride<R, TPD, (W >= (int)TPD) ? W / TPD : 0>();
     __shared__ uint32_t s_cnt[W * RS + 1];                                       // + padding counter
-    __shared__ uint2 s_out[R];        // per digit: {global - LDS key index, first line << 8 | first valid lane}
+    // per digit: {global - LDS key index, first line << 8 | first valid lane} (+ with next-digit counts, s_nb's
+    // position: one LDS read per output quad gets both)
+    typedef typename std::conditional<(R <= 16) && DMODE == kDigitShift, uint4, uint2>::type OutRec;
+    __shared__ OutRec s_out[R];
     __shared__ uint2 s_flush[R];      // chunk end: {A, inv | carry << 8}
     __shared__ uint32_t s_ws[W];
     // Next-digit counts (k <= 4 with a.next_table): the NEXT pass's chunk table, counted here by
@@ -1941,7 +1945,7 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
     const uint32_t sub = t % TPD;
     const bool leader = sub == 0;
     const uint32_t glead = lane & ~(TPD - 1u);
-    uint32_t g_run = 0, carry = 0, inv = 0;
+    uint32_t g_run = 0, carry = 0, inv = 0, nb_own = 0;  // (nb_own: the leader's s_nb entry)
     const uint32_t base = w * SEG + lane;
     auto load_tile = [&](uint64_t tb, uint32_t (&k)[KPT], uint32_t (&v)[PAIRS ? KPT : 1]) {
         const uint32_t valid = (uint32_t)min<uint64_t>((uint64_t)T, cend - tb);
@@ -2004,7 +2008,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
             if (count_next) {
                 const uint64_t oc = (uint64_t)g0 / a.chunk_keys;  // (the next pass's chunks: unshifted)
                 s_oc[d_own] = (uint32_t)oc;
-                s_nb[d_own] = (uint32_t)min<uint64_t>((oc + 1) * a.chunk_keys, 0xFFFFFFFFull);
+                nb_own = (uint32_t)min<uint64_t>((oc + 1) * a.chunk_keys, 0xFFFFFFFFull);
+                s_nb[d_own] = nb_own;
             }
         }
     }
@@ -2021,17 +2026,26 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
 
     // one 16-B quad of line L at quad offset q -> global; every key of an LDS line has the line's
     // digit, which locates the line's segment record (info)
-    auto store_quad = [&](uint32_t L, uint32_t q, const u32x4 &kv, const u32x4 &vv, const uint2 &info, uint32_t d) {
+    auto store_quad = [&](uint32_t L, uint32_t q, const u32x4 &kv, const u32x4 &vv, const OutRec &info, uint32_t d) {
         const uint32_t lo = (info.y >> 8) == L ? (info.y & 0xFFu) : 0u;
         const uint64_t gp = (uint64_t)(info.x + L * G + q);
         if constexpr (NX) {
             if (count_next) {
                 // (per element: with a pos_shift that is not a multiple of 4 a quad can straddle a
-                // chunk boundary of the unshifted positions)
+                // chunk boundary of the unshifted positions). s_nb[d] comes with the digit's record: read
+                // inside the element loop it was re-read after every add (the adds may alias it), each
+                // read a full LDS round trip the adds then waited for (k = 4 middle passes, dev/LOG.md)
                 const uint32_t p0 = (uint32_t)gp - a.pos_shift;
+                uint32_t nbd;
+                if constexpr (NX) nbd = info.z;
+                if (lo <= q) {  // (every element: all but a chunk's first line)
 #pragma unroll
-                for (uint32_t x = 0; x < 4; ++x)
-                    if (lo <= q + x) next_add(d, p0 + x >= s_nb[d] ? 1u : 0u, kv[x]);
+                    for (uint32_t x = 0; x < 4; ++x) next_add(d, p0 + x >= nbd ? 1u : 0u, kv[x]);
+                } else {
+#pragma unroll
+                    for (uint32_t x = 0; x < 4; ++x)
+                        if (lo <= q + x) next_add(d, p0 + x >= nbd ? 1u : 0u, kv[x]);
+                }
             }
         }
         if (lo <= q) {
@@ -2068,8 +2082,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
             if (two) vv1 = *reinterpret_cast<const u32x4 *>(&s_vstage[L1 * G + q1]);
         }
         const uint32_t d0 = dig(kv0.x), d1 = dig(kv1.x);
-        const uint2 in0 = s_out[d0];
-        const uint2 in1 = s_out[d1];
+        const OutRec in0 = s_out[d0];
+        const OutRec in1 = s_out[d1];
         store_quad(L0, q0, kv0, vv0, in0, d0);
         if (two) store_quad(L1, q1, kv1, vv1, in1, d1);
     };
@@ -2238,7 +2252,8 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
                 }
             }
             if (leader) {
-                s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
+                if constexpr (NX) s_out[d] = make_uint4(gA - gS, ((gS / G) << 8) | ginv, nb_own, 0u);
+                else s_out[d] = make_uint2(gA - gS, ((gS / G) << 8) | ginv);
                 if (gw > 0) inv = 0;
                 carry = e - (A + gw);  // pending - written
                 g_run = e;
