@@ -261,15 +261,17 @@ def _run_loopback(world, inputs, k, capacity=None, piece=None, opts=0, stats=Non
 @pytest.mark.parametrize("world,dist_name,pairs,k,piece", [(2, "uniform", False, 8, None), (2, "zipf", True, 8, None),
                                                            (3, "hot", True, 8, 4096), (4, "equal", False, 8, None),
                                                            (4, "uniform", True, 4, 10000), (8, "zipf", False, 8, None),
-                                                           (3, "empty0", True, 8, None)])
+                                                           (3, "empty0", True, 8, None), (12, "hot", True, 8, None),
+                                                           (16, "zipf", True, 8, None)])
 def test_c_multi_loopback(world, dist_name, pairs, k, piece):
-    """rsort_u32_multi_transport at world 2..8 with the real kernels (sampling, device sort of the
+    """rsort_u32_multi_transport at world 2..16 with the real kernels (sampling, device sort of the
     gathered sample, partition into equal-key buckets, exchange plan, exchange, in-place local
     sort): the ranks' outputs concatenated in rank order equal Baseline1 on the union of the
     inputs (stable with values), offsets are the exclusive scan of the counts, and every rank
-    holds the mean count within 5 % -- also when one key holds 3/4 of the keys. piece: keys per
-    exchange message (rsort_set_exchange_piece), small to force many rounds."""
-    n = 300_000
+    holds the mean count within 5 % -- also when one key holds 3/4 of the keys, and at world 12 and 16,
+    whose hot quantile keys take the partition past 16 buckets. piece: keys per exchange message
+    (rsort_set_exchange_piece), small to force many rounds."""
+    n = 300_000 if world <= 8 else 100_000
     inputs = [_loopback_inputs(r, n, dist_name, pairs) for r in range(world)]
     res = _run_loopback(world, inputs, k, piece=piece)
     assert all(isinstance(x, tuple) for x in res), res
