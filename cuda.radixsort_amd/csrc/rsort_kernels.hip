@@ -110,10 +110,12 @@ __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) -
 // Lane count of a wave-uniform mask as an opaque 32-bit scalar. `__popcll(m) < c` is folded into a
 // 64-bit unsigned compare of the i64 popcount, which the SALU cannot do (no s_cmp_lt_u64): it went
 // to the VALU (v_cmp_lt_u64 on SGPR operands) on every key of the rank loops. s_bcnt1 into a 32-bit
-// SGPR keeps the test on the SALU (s_cmp + s_cbranch_scc).
+// SGPR keeps the test on the SALU (s_cmp + s_cbranch_scc). s_bcnt1 also writes SCC: declared, or the
+// compiler may place it between another compare and the branch on that compare (it did, round 6: a
+// tile's rank-check test `tno & 7` branched on this count instead).
 __device__ __forceinline__ uint32_t wave_count(uint64_t m) {
     uint32_t c;
-    asm("s_bcnt1_i32_b64 %0, %1" : "=s"(c) : "s"(m));
+    asm("s_bcnt1_i32_b64 %0, %1" : "=s"(c) : "s"(m) : "scc");
     return c;
 }
 
@@ -2088,6 +2090,9 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
         if (two) store_quad(L1, q1, kv1, vv1, in1, d1);
     };
 
+    // CL = 2 with split digits: the few-bucket ranking (launch_scatter picks it for nsplit < 4)
+    constexpr bool FEW = DMODE == kDigitSplit && CL == 2;
+    static_assert(CL != 2 || FEW, "CL = 2: split digits only");
     uint32_t hotd = 0xFFFFFFFFu;  // CL: the wave's last aggregated digit (none yet)
     uint32_t order_bad = 0;       // the per-tile rank check (rank_check) failed in this thread
 
@@ -2134,6 +2139,29 @@ __global__ __launch_bounds__(THREADS, THREADS == 256 ? hooks::kLinesMinWavesSmal
                     rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
                 }
             }
+        } else if (full && FEW) {
+            // partitions into <= 4 buckets (CL = 2, launch_scatter): 16-32 lanes of a slot share each digit,
+            // and lane-ordered adds serialised them on one LDS counter (2^30 keys into 2 buckets: 2.8 ms
+            // against 1.8 for 8). Here the wave's running count of each digit is a wave-uniform register:
+            // a key's rank is its digit's count plus the lanes below with the same digit (one ballot per
+            // digit); the counts go to the wave's counter row after the tile
+            uint32_t c4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t dj = dig(key[j]);
+                if constexpr (PD) dpk[j / 8] |= dj << (4 * (j % 8));
+                uint32_t r = 0;
+#pragma unroll
+                for (uint32_t v = 0; v < 4; ++v) {
+                    const uint64_t m = __ballot(dj == v);
+                    if (dj == v)
+                        r = c4[v] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    c4[v] += wave_count(m);
+                }
+                if (j == 0 && check_tile) order_bad |= rank_check<BITS>(dj, r, a.rank_fault);
+                rk[j / 2] = (j & 1) ? (rk[j / 2] | (r << 16)) : r;
+            }
+            if (lane < 4u) s_cnt[w * RS + lane] = lane == 0u ? c4[0] : lane == 1u ? c4[1] : lane == 2u ? c4[2] : c4[3];
         } else if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
@@ -3155,6 +3183,21 @@ hipError_t launch_scatter(int bits, int pairs, int rank_algo, int dmode, int geo
         constexpr int TH = kGeomShape[kGeomSmall].threads, KP = kGeomShape[kGeomSmall].kpt;
         fn = bits == 3 ? reg_lines<3, TH, KP, kLineKeys, false, kDigitShift, 1>()
                        : reg_lines<4, TH, KP, kLineKeys, false, kDigitShift, 1>();
+    }
+    // partitions into <= 4 buckets: the line kernel's few-bucket ranking instance (CL = 2)
+    if (dmode == kDigitSplit && a.nsplit < 4u) {
+        constexpr int ST = kGeomShape[kGeomSmall].threads, SK = kGeomShape[kGeomSmall].kpt;
+        constexpr int KT = kGeomShape[kGeomK4].threads, KK = kGeomShape[kGeomK4].kpt;
+        if (fn == reinterpret_cast<void *>(&rs_scatter_lines<2, ST, SK, kLineKeys, false, kDigitSplit, 3>))
+            fn = reg_lines<2, ST, SK, kLineKeys, false, kDigitSplit, 3, 2>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<3, ST, SK, kLineKeys, false, kDigitSplit, 3>))
+            fn = reg_lines<3, ST, SK, kLineKeys, false, kDigitSplit, 3, 2>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<2, ST, SK, kLineKeysPairs, true, kDigitSplit, 2>))
+            fn = reg_lines<2, ST, SK, kLineKeysPairs, true, kDigitSplit, 2, 2>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<3, ST, SK, kLineKeysPairs, true, kDigitSplit, 2>))
+            fn = reg_lines<3, ST, SK, kLineKeysPairs, true, kDigitSplit, 2, 2>();
+        else if (fn == reinterpret_cast<void *>(&rs_scatter_lines<3, KT, KK, kLineKeys, false, kDigitSplit, 3>))
+            fn = reg_lines<3, KT, KK, kLineKeys, false, kDigitSplit, 3, 2>();
     }
     // clustered-input variants of the k = 8 line kernels (rank_add_hot): both kernels are launched,
     // the device-side flag *cl_select picks the one that works (the other leaves at once: ~3 us)
