@@ -424,7 +424,7 @@ RSORT_API int rsort_set_comm_timeout(int timeout_ms);
  *  Neither: the overlap runs for 2 <= world <= 8 (RSORT_MULTI_AUTO_OVERLAP_MAX_WORLD; 2 x world <=
  *                       RSORT_MAX_RANKS virtual ranks), where it is predicted faster at every size
  *                       (components measured on one GPU; at world 8 the partition into
- *                       16 buckets costs 2.40 ms against 2.49 ms for 8).
+ *                       16 buckets costs 2.49 ms, as the 8 buckets without halves).
  *  RSORT_MULTI_FULL     run the whole protocol also at world 1 (sample, partition into one
  *                       bucket, self exchange): for tests and overhead measurements. By default
  *                       one rank sorts its keys directly (the partition would be a copy). */
