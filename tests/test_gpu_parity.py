@@ -417,7 +417,8 @@ def _cus():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
-@pytest.mark.parametrize("nb,repeat", [(2, False), (8, True), (15, True), (16, False), (31, True), (32, False)])
+@pytest.mark.parametrize("nb,repeat", [(1, False), (2, False), (3, False), (4, True), (8, True), (15, True), (16, False),
+                                       (31, True), (32, False)])
 def test_partition_stable_large(nb, repeat):
     """keys-only partitions of n >= 2 x CUs x 8192 keys run the 512 x 16 line tiles with
     splitter digits (rsort_capi.cpp choose_geom). n = 2 x CUs x 8192 + odd, Zipf keys; with
