@@ -504,6 +504,49 @@ def test_partition_prefix_table(case, size):
     assert np.array_equal(host(starts), exp)
 
 
+def test_partition_fuzz():
+    """60 random partitions (seeded): 1..32 buckets, splitters drawn uniformly, from a few prefixes or
+    from the keys themselves (so some repeat), keys and pairs, small and 512 x 16-tile sizes -- every split
+    digit path (compares, register counts, the prefix table with spans of 0..7+, the few-bucket ranking)
+    against numpy's stable argsort of searchsorted(side='right') buckets."""
+    rng = np.random.default_rng(20261018)
+    big = 2 * _cus() * 8192 + 333
+    for trial in range(60):
+        nb = int(rng.integers(1, 33))
+        n = int(rng.choice([1, 97, 4096 * 3 + 5, 65537, big]))
+        mode = trial % 3
+        x = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+        if mode == 0:
+            split = rng.integers(0, 1 << 32, size=nb - 1)
+        elif mode == 1:  # splitters crowded into two 2^21-key prefixes, half the keys next to them
+            p = rng.integers(0, 1 << 11, size=2) << 21
+            split = p[rng.integers(0, 2, size=nb - 1)] + rng.integers(0, 1 << 21, size=nb - 1)
+            if nb > 1:
+                near = split[rng.integers(0, nb - 1, size=n // 2)] + rng.integers(-2, 3, size=n // 2)
+                x[: n // 2] = np.clip(near, 0, 0xFFFFFFFF).astype(np.uint32)
+        else:  # splitters are keys (repeats likely with a small key set)
+            x = rng.choice((np.arange(40, dtype=np.int64) * 0x06000001) & 0xFFFFFFFF, size=n).astype(np.uint32)
+            split = rng.choice(x, size=nb - 1).astype(np.int64)
+        split = np.sort(np.clip(split, 0, 0xFFFFFFFF)).astype(np.uint32)
+        bucket = np.searchsorted(split, x, side="right")
+        order = np.argsort(bucket, kind="stable")
+        pairs = trial % 4 == 1
+        ko = rs.empty_u32(n)
+        starts = rs.empty_u32(nb + 1)
+        if pairs:
+            v = np.arange(n, dtype=np.uint32)
+            vo = rs.empty_u32(n)
+            rs.partition_device(dev(x), ko, split.tolist(), starts, vals_in=dev(v), vals_out=vo)
+        else:
+            rs.partition_device(dev(x), ko, split.tolist(), starts)
+        torch.cuda.synchronize()
+        assert np.array_equal(host(ko), x[order]), (trial, nb, n, mode)
+        if pairs:
+            assert np.array_equal(host(vo), v[order]), (trial, nb, n, mode)
+        exp = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nb))]).astype(np.uint32)
+        assert np.array_equal(host(starts), exp), (trial, nb, n, mode)
+
+
 def test_plan_check_and_kernels_used():
     """rsort_plan_check reports the tail scans' self-check (0 = every next-pass table summed to n)
     after k = 3, 4 sorts; rsort_scatter_kernels_used names what the dispatch launched."""
