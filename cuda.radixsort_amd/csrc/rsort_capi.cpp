@@ -320,7 +320,9 @@ int do_histogram_joint(const rsort_plan &p, const uint32_t *keys, int shift, uin
     // the first joint count of a sort clears the counts; a later one finds them cleared by the
     // copy-mode histogram that used them (or, where that pass fell back, is disabled by `enable`)
     // (the rows counter sits after the joint counts: cleared with them)
-    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4 + 4, s) != hipSuccess)
+    // (16 bytes past the counts, inside the 256-B-aligned region: a fill of a multiple of 16 bytes is one
+    // kernel, the 4-byte tail of an odd size was a second one, ~5 us per sort)
+    if (zero_joint && hipMemsetAsync(joint, 0, (size_t)kJointBins * kJointBins * 4 + 16, s) != hipSuccess)
         return RSORT_ERR_HIP;
     return hip_status(launch_histogram_joint(a, s));
 }
